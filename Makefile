@@ -1,0 +1,51 @@
+# Build for MI355X (gfx950) only. Outputs stay in-tree so they travel to the GPU box with gpurun.
+#   make            -> genomicsbench_palisade_amd/lib/libgb.so (C ABI: gb_*), libgkl_pairhmm_c.so
+#                      (reference-compatible drop-in), bin/phmm, oracle/_build/liboracle.so
+#   make ref        -> also oracle/_ref/* (reference kernels; needs /root/reference)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := genomicsbench_palisade_amd
+CSRC := $(PKG)/csrc
+LIB := $(PKG)/lib
+BIN := $(PKG)/bin
+# -ffp-contract=off is part of the arithmetic contract (no FMA anywhere).
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
+HOSTCXX := g++
+HOSTFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off -Wall
+
+HIP_SRCS := $(wildcard $(CSRC)/*.hip)
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(LIB)/obj/%.o,$(HIP_SRCS)) $(LIB)/obj/gb_common.o
+HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
+
+.PHONY: all ref clean oracle
+all: $(LIB)/libgb.so $(LIB)/libgkl_pairhmm_c.so $(BIN)/phmm oracle
+
+$(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(LIB)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB)/obj/gb_common.o: $(CSRC)/gb_common.cpp $(HDRS)
+	@mkdir -p $(LIB)/obj
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB)/libgb.so: $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+
+# Reference-compatible drop-in: exports initPairHMM()/computelikelihoodsboth() with the reference's
+# C++ linkage (IntelPairHmmCSource.cpp:29-115) on top of libgb.so.
+$(LIB)/libgkl_pairhmm_c.so: $(CSRC)/gkl_dropin.cpp $(LIB)/libgb.so $(HDRS)
+	$(HOSTCXX) $(HOSTFLAGS) -shared -o $@ $< -L$(LIB) -lgb -Wl,-rpath,'$$ORIGIN'
+
+$(BIN)/phmm: $(PKG)/drivers/phmm_main.cpp $(LIB)/libgb.so
+	@mkdir -p $(BIN)
+	$(HOSTCXX) $(HOSTFLAGS) -pthread -o $@ $< -L$(LIB) -lgb -Wl,-rpath,'$$ORIGIN/../lib'
+
+oracle:
+	$(MAKE) -s -C oracle all
+
+ref:
+	$(MAKE) -s -C oracle ref
+
+clean:
+	rm -rf $(LIB) $(BIN)
+	$(MAKE) -s -C oracle clean

@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py -- GenomicsBench hot kernels on MI355X (driver contract: one JSON line on rank 0).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batches B] [--no-cpu-baseline]
+
+Metric (BASELINE.json): "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X".
+A step = one PairHMM forward pass (f32 kernel + f64 fallback kernel + log10 epilogue) over one
+'large'-shaped synthetic job of B batches (gen.phmm_dataset, seed 1 + rank) already resident in HBM.
+`value` = total cells of all ranks x K / max-over-ranks wall time of the K timed steps, in GCUPS.
+Weak scaling: every rank processes its own job of the same shape (independent shards, no
+data-path collective; torch.distributed only provides the barrier and the max-time reduction).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Peaks (MI355X_MICROARCH.md, chip-level parameters): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+PEAK_F32_OPS = 256 * 4 * 32 * 2.4e9  # non-FMA FP32 VALU ops/s = 78.6e12 (157.3 TF counts FMA as 2)
+PEAK_F64_OPS = PEAK_F32_OPS / 2      # FP64 vector peak 78.6 TF (FMA=2) -> 39.3e12 non-FMA ops/s
+PHMM_FLOP_PER_CELL = 12              # 12 FP ops per cell, no FMA
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return world, rank, local
+
+
+class Dist:
+    def __init__(self, world):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group(backend="gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def device_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def cpu_baseline_phmm(ta, sample_seconds: float):
+    """Reference GKL kernels (oracle/_ref, kind 'reference') -- or the C restatement when the
+    reference build is absent (kind 'port') -- on a bounded random sample of the same job."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: F401
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))  # the GPU box grants 16 CPUs per GPU
+    ref = oracle_lib.ref_phmm()
+    rng = np.random.default_rng(123)
+    order = rng.permutation(ta.n)
+    kind = "reference" if ref is not None else "port"
+    engine = 512 if (ref is not None and ref.ref_phmm_has_avx512()) else 256
+
+    def run(sub):
+        n = sub.n
+        out, rf, rd = np.zeros(n), np.zeros(n, np.float32), np.zeros(n)
+        t0 = time.perf_counter()
+        if ref is not None:
+            ref.ref_phmm_batch(ctypes.addressof(sub.arr), n, out.ctypes.data, rf.ctypes.data,
+                               rd.ctypes.data, engine, threads)
+        else:
+            oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(sub.arr), n, out.ctypes.data,
+                                                  rf.ctypes.data, rd.ctypes.data, None, threads)
+        return time.perf_counter() - t0
+
+    # calibrate on a small sample, then size the timed sample to ~sample_seconds
+    cal = ta.subset(order[:max(threads * 8, 64)])
+    t = run(cal)
+    rate = cal.cells() / max(t, 1e-6)
+    ncells_target = rate * sample_seconds
+    cum = np.cumsum(ta.np_arr["rslen"][order].astype(np.int64) * ta.np_arr["haplen"][order])
+    m = int(min(ta.n, max(64, np.searchsorted(cum, ncells_target))))
+    sub = ta.subset(order[:m])
+    t = run(sub)
+    gcups = sub.cells() / t / 1e9
+    eng = {512: "AVX-512", 256: "AVX2"}[engine] if ref is not None else "C"
+    return {"value": gcups, "unit": "GCUPS", "cores": threads, "kind": kind,
+            "sample": f"{m} of {ta.n} testcases ({sub.cells() / 1e9:.2f} G cells, random) of the same "
+                      f"job, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batches", type=int, default=16, help="'large' batches per job (per rank)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    D = Dist(world)
+    import genomicsbench_palisade_amd as gb
+    from genomicsbench_palisade_amd import gen, phmm
+    from genomicsbench_palisade_amd._tc import TestcaseArray
+
+    gb.set_device(local)
+    phmm.init_pairhmm()
+    batches = gen.phmm_dataset("large", args.batches, seed=1 + rank)
+    ta = TestcaseArray.from_batches(batches)
+    job = phmm.DeviceBatch(ta)
+    ntc, cells, _ = job.stats()
+
+    for _ in range(args.warmup):
+        job.run()
+        job.sync()
+    _, rf, _, used, _ = job.results()
+    rl = ta.np_arr["rslen"][:ta.n].astype(np.int64)
+    hl = ta.np_arr["haplen"][:ta.n].astype(np.int64)
+    cells_f64 = int((rl * hl)[used.astype(bool)].sum())
+
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    k32, k64 = [], []
+    for _ in range(args.steps):
+        job.run()
+        job.sync()
+        a, b, _ = job.timing()
+        k32.append(a)
+        k64.append(b)
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    total_cells = D.sum(float(cells)) * args.steps
+    gcups = total_cells / elapsed / 1e9
+
+    ms32, ms64 = float(np.mean(k32)), float(np.mean(k64))
+    if ms32 >= ms64:
+        kern, ach, peak = "phmm_forward<float>", PHMM_FLOP_PER_CELL * cells / (ms32 * 1e-3), PEAK_F32_OPS
+    else:
+        kern, ach, peak = "phmm_forward<double>", PHMM_FLOP_PER_CELL * cells_f64 / (ms64 * 1e-3), PEAK_F64_OPS
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X",
+            "value": round(gcups, 3),
+            "unit": "GCUPS (phmm)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": "synthetic ('large'-shaped PairHMM batches, gen.phmm_dataset seed 1+rank)",
+            "config": {"workload": "phmm large: %d batches/rank, %d testcases, %.3f G cells/rank/step,"
+                                   " %.1f%% testcases on the f64 fallback" % (
+                                       args.batches, ntc, cells / 1e9, 100.0 * used.mean()),
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
+                         "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": None},
+            "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    job.close()
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+// gkl_dropin.cpp -- libgkl_pairhmm_c.so replacement: the reference's C++ entry points
+// (IntelPairHmmCSource.cpp:29-115) implemented over the gb_phmm C ABI (MI355X kernels).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/gb_phmm.h"
+#include "../../include/gkl_pairhmm_c.h"
+
+static_assert(sizeof(testcase) == sizeof(gb_testcase), "testcase layout must match gb_testcase");
+
+static void die(const char *what, int st) {
+  fprintf(stderr, "[gkl_pairhmm_c/MI355X] %s failed (%d): %s\n", what, st, gb_last_error());
+  abort();
+}
+
+void initPairHMM() {
+  const char *dev = getenv("GB_DEVICE");
+  int st = gb_set_device(dev ? atoi(dev) : 0);
+  if (st) die("gb_set_device", st);
+  st = gb_phmm_init();
+  if (st) die("gb_phmm_init", st);
+  printf("MI355X (gfx950) PairHMM initialized\n");
+}
+
+void computelikelihoodsboth(testcase *testcases, double *expected_results, int batch_size) {
+  int st = gb_phmm_compute(reinterpret_cast<const gb_testcase *>(testcases), batch_size,
+                           expected_results, nullptr, nullptr, nullptr);
+  if (st) die("gb_phmm_compute", st);
+  // The reference prints every result (IntelPairHmmCSource.cpp:80); opt-in here.
+  static const int print = getenv("GB_PHMM_PRINT_RESULTS") ? atoi(getenv("GB_PHMM_PRINT_RESULTS")) : 0;
+  if (print)
+    for (int i = 0; i < batch_size; i++) printf("i: %d; result_final: %f\n", i, expected_results[i]);
+}
+
+void computelikelihoodsfloat(testcase *testcases, float *expected_result) {
+  // f32 probability only (no f64 fallback), as IntelPairHmmCSource.cpp:89-99
+  float rf = 0.f;
+  double res = 0.0;
+  int st = gb_phmm_compute(reinterpret_cast<const gb_testcase *>(testcases), 1, &res, &rf, nullptr,
+                           nullptr);
+  if (st) die("gb_phmm_compute", st);
+  *expected_result = (float)(double)(log10f(rf) - log10f(ldexpf(1.f, 120)));
+}
+
+void computelikelihoodsdouble(testcase *testcases, double *expected_result) {
+  // f64 probability (IntelPairHmmCSource.cpp:103-115): force the f64 pass via the raw value.
+  float rf = 0.f;
+  double rd = 0.0, res = 0.0;
+  uint8_t used = 0;
+  int st = gb_phmm_compute(reinterpret_cast<const gb_testcase *>(testcases), 1, &res, &rf, &rd, &used);
+  if (st) die("gb_phmm_compute", st);
+  if (!used) {
+    st = gb_phmm_compute_f64(reinterpret_cast<const gb_testcase *>(testcases), 1, &rd);
+    if (st) die("gb_phmm_compute_f64", st);
+  }
+  *expected_result = log10(rd) - log10(ldexp(1.0, 1020));
+}

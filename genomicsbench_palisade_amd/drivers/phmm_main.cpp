@@ -1,0 +1,187 @@
+// phmm_main.cpp -- `phmm` benchmark driver, CLI-compatible with the reference
+// (benchmarks/phmm/PairHMMUnitTest_orig.cpp; HE fork benchmarks/phmm/PairHMMUnitTest.cpp:650-771):
+//   phmm -f <file.in> [-l loops] [-t threads] [-g gpus] [-p]
+// Input format and normalization follow read_batch (PairHMMUnitTest.cpp:118-210,461-474):
+//   "R H", then R lines "bases q i d c" (q: max(6, x-33); i/d/c: max(0, x-33)), then H haplotypes.
+// MI355X-first difference: all batches of the file are merged into one device-resident job per GPU
+// (testcases of every batch in r-major order), so small batches do not starve the GPU; results are
+// scattered back per batch. With -g N the batches are sharded over N GPUs by cells (one host thread
+// per device, no collective). Prints the reference's closing line "PairHMM completed. Kernel
+// runtime: X sec"; -p prints every result like PRINT_OUTPUT ("%lf").
+#include <getopt.h>
+#include <sys/time.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/gb_phmm.h"
+#include "../../include/gkl_pairhmm_c.h"
+
+namespace {
+
+struct ReadRec {
+  std::string bases, q, i, d, c;
+};
+struct Batch {
+  std::vector<ReadRec> reads;
+  std::vector<std::string> haps;
+  std::vector<double> results;
+  long long cells = 0;
+};
+
+void normalize(std::string &s, int min_value = 0) {
+  for (auto &ch : s) ch = (char)std::max(min_value, (int)ch - 33);
+}
+
+bool read_batch(std::istream &is, Batch &b) {
+  int R = 0, H = 0;
+  if (!(is >> R >> H)) return false;
+  is >> std::ws;
+  b.reads.resize(R);
+  long long tr = 0, th = 0;
+  for (int r = 0; r < R; r++) {
+    ReadRec &x = b.reads[r];
+    is >> x.bases >> x.q >> x.i >> x.d >> x.c >> std::ws;
+    normalize(x.q, 6);
+    normalize(x.i);
+    normalize(x.d);
+    normalize(x.c);
+    tr += (long long)x.bases.size();
+  }
+  b.haps.resize(H);
+  for (int h = 0; h < H; h++) {
+    is >> b.haps[h] >> std::ws;
+    th += (long long)b.haps[h].size();
+  }
+  b.cells = tr * th;
+  b.results.assign((size_t)R * H, 0.0);
+  return true;
+}
+
+void die(const char *what, int st) {
+  fprintf(stderr, "phmm: %s failed (%d): %s\n", what, st, gb_last_error());
+  exit(EXIT_FAILURE);
+}
+
+// Runs the given batches as one device-resident job on `device`; returns kernel seconds.
+double run_shard(int device, std::vector<Batch *> shard, int loops) {
+  if (shard.empty()) return 0.0;
+  int st = gb_set_device(device);
+  if (st) die("gb_set_device", st);
+  st = gb_phmm_init();
+  if (st) die("gb_phmm_init", st);
+  std::vector<gb_testcase> tcs;
+  for (Batch *b : shard)
+    for (auto &r : b->reads)
+      for (auto &h : b->haps) {
+        gb_testcase t;
+        t.rslen = (int)r.bases.size();
+        t.haplen = (int)h.size();
+        t.hap = h.c_str();
+        t.rs = r.bases.c_str();
+        t.q = r.q.c_str();
+        t.i = r.i.c_str();
+        t.d = r.d.c_str();
+        t.c = r.c.c_str();
+        tcs.push_back(t);
+      }
+  gb_phmm_batch *job = nullptr;
+  st = gb_phmm_batch_create(tcs.data(), (int)tcs.size(), &job);
+  if (st) die("gb_phmm_batch_create", st);
+  std::vector<double> res(tcs.size());
+  struct timeval t0, t1;
+  gettimeofday(&t0, nullptr);
+  for (int l = 0; l < loops; l++) {
+    st = gb_phmm_batch_run(job);
+    if (st) die("gb_phmm_batch_run", st);
+  }
+  st = gb_phmm_batch_results(job, res.data(), nullptr, nullptr, nullptr, nullptr);
+  if (st) die("gb_phmm_batch_results", st);
+  gettimeofday(&t1, nullptr);
+  gb_phmm_batch_destroy(job);
+  size_t k = 0;
+  for (Batch *b : shard)
+    for (auto &v : b->results) v = res[k++];
+  return (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  static const char *usage =
+      "  -f, --testfile                       name of test file\n"
+      "  -l, --loop                           number of loops\n"
+      "  -t  --threads                        number of host threads (parsing; kept for compatibility)\n"
+      "  -g  --gpus                           number of MI355X devices to shard over (default 1)\n"
+      "  -p  --print                          print every result (PRINT_OUTPUT)\n";
+  static const struct option longopts[] = {{"testfile", required_argument, nullptr, 'f'},
+                                           {"loop", required_argument, nullptr, 'l'},
+                                           {"threads", required_argument, nullptr, 't'},
+                                           {"gpus", required_argument, nullptr, 'g'},
+                                           {"print", no_argument, nullptr, 'p'},
+                                           {nullptr, 0, nullptr, 0}};
+  if (argc == 1) {
+    std::cout << usage;
+    return EXIT_FAILURE;
+  }
+  std::string testfile;
+  int loops = 1, gpus = 1;
+  bool print = false;
+  for (int c; (c = getopt_long(argc, argv, "f:l:t:g:p", longopts, nullptr)) != -1;) {
+    switch (c) {
+      case 'f': testfile = optarg; break;
+      case 'l': loops = std::max(1, atoi(optarg)); break;
+      case 't': break;
+      case 'g': gpus = std::max(1, atoi(optarg)); break;
+      case 'p': print = true; break;
+      default: std::cout << usage; return EXIT_FAILURE;
+    }
+  }
+  setbuf(stdout, nullptr);
+  std::ifstream ifs(testfile);
+  if (!ifs.is_open()) {
+    printf("Cannot open file : %s", testfile.c_str());
+    return 0;
+  }
+  std::vector<Batch> batches;
+  while (true) {
+    Batch b;
+    if (!read_batch(ifs, b)) break;
+    batches.push_back(std::move(b));
+  }
+  int ndev = 0;
+  if (gb_device_count(&ndev)) die("gb_device_count", GB_ERR_NODEV);
+  gpus = std::min(gpus, ndev);
+  printf("Num Batches %zu, Num GPUs %d\n", batches.size(), gpus);
+
+  // Shard whole batches over GPUs, balanced by cells (largest first onto the lightest shard).
+  std::vector<std::vector<Batch *>> shards(gpus);
+  std::vector<long long> load(gpus, 0);
+  std::vector<size_t> idx(batches.size());
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return batches[a].cells > batches[b].cells; });
+  for (size_t i : idx) {
+    int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    shards[g].push_back(&batches[i]);
+    load[g] += batches[i].cells;
+  }
+  for (auto &s : shards)
+    std::sort(s.begin(), s.end());  // keep file order inside a shard
+  std::vector<double> secs(gpus, 0.0);
+  std::vector<std::thread> th;
+  for (int g = 0; g < gpus; g++) th.emplace_back([&, g] { secs[g] = run_shard(g, shards[g], loops); });
+  for (auto &t : th) t.join();
+  double runtime = *std::max_element(secs.begin(), secs.end());
+  if (print)
+    for (auto &b : batches)
+      for (double v : b.results) printf("%lf\n", v);
+  printf("\nPairHMM completed. Kernel runtime: %.2f sec\n", runtime);
+  return 0;
+}

@@ -1,0 +1,126 @@
+"""Regenerate the committed golden vectors from the REFERENCE kernels (oracle/_ref, built from
+/root/reference by `make -C oracle ref`). Run in the build container only:
+
+    python tests/golden/make_golden.py
+
+phmm_golden.npz: reads x haps cross product + edge pairs, expected outputs of the reference GKL
+AVX2 kernels (compute_fp_avxs/avxd) driven like computelikelihoodsboth
+(IntelPairHmmCSource.cpp:61-85): raw f32 bits, raw f64 bits (0 unless the f64 fallback ran) and
+the final log10 likelihood bits. The AVX-512 kernels are cross-checked to agree bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from genomicsbench_palisade_amd import gen  # noqa: E402
+from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: E402
+import oracle_lib  # noqa: E402
+
+
+def phmm_inputs(seed=2024):
+    rng = np.random.default_rng(seed)
+    reads, haps = [], []
+    # cross-product block: 40 reads x 25 haps, lengths chosen to hit stripe edges (64k, 64k+1)
+    rlens = [1, 2, 7, 63, 64, 65, 100, 127, 128, 129, 150, 191, 192, 193, 250, 255, 256, 257, 300]
+    while len(rlens) < 40:
+        rlens.append(int(rng.integers(1, 320)))
+    hlens = [1, 2, 5, 64, 100, 150, 200, 255, 302, 473, 511, 600]
+    while len(hlens) < 25:
+        hlens.append(int(rng.integers(1, 700)))
+    src = gen.BASES[rng.integers(0, 4, 1200)]
+    for hl in hlens:
+        off = int(rng.integers(0, 400))
+        h = gen._mutate(rng, src[off:off + hl], 0.03, 0.01)
+        haps.append(h.tobytes())
+    alphabet = np.frombuffer(b"ACGTNacgtX", dtype=np.uint8)
+    for k, rl in enumerate(rlens):
+        off = int(rng.integers(0, 400))
+        b = src[off:off + rl].copy()
+        sub = rng.random(rl) < [0.0, 0.02, 0.1, 0.3][k % 4]
+        b[sub] = gen.BASES[rng.integers(0, 4, sub.sum())]
+        if k % 5 == 4:  # exotic bytes: lowercase and unknown letters behave like 'A'
+            ex = rng.random(rl) < 0.05
+            b[ex] = alphabet[rng.integers(0, len(alphabet), ex.sum())]
+        nm = rng.random(rl) < 0.02
+        b[nm] = ord("N")
+        if k % 7 == 3:   # full quality range incl. >=128 (only the low 7 bits count, &127)
+            q = rng.integers(0, 256, rl)
+            i = rng.integers(0, 256, rl)
+            d = rng.integers(0, 256, rl)
+            c = rng.integers(0, 256, rl)
+        else:
+            q = rng.integers(6, 41, rl)
+            i = rng.integers(10, 60, rl)
+            d = rng.integers(10, 60, rl)
+            c = rng.integers(5, 20, rl)
+        reads.append(tuple(np.asarray(x, np.uint8).tobytes() for x in (b, q, i, d, c)))
+    # explicit pairs: the GKL KAT (PairHmmUnitTest.java:23-56) and tiny corner cases
+    plus = b"+" * 4
+    pairs = [((b"ACGT", plus, plus, plus, plus), b"ACGT"),
+             ((b"A", b"\x06", b"\x2d", b"\x2d", b"\x0a"), b"A"),
+             ((b"A", b"\x06", b"\x2d", b"\x2d", b"\x0a"), b"C"),
+             ((b"N", b"\x28", b"\x2d", b"\x2d", b"\x0a"), b"G"),
+             ((b"ACGTACGT", b"\x00" * 8, b"\x00" * 8, b"\x00" * 8, b"\x00" * 8), b"TTTTTTTTTTTT"),
+             ((b"G" * 70, b"\x7f" * 70, b"\x7f" * 70, b"\x7f" * 70, b"\x7f" * 70), b"G" * 70),
+             ((b"C" * 200, b"\x28" * 200, b"\x2d" * 200, b"\x2d" * 200, b"\x0a" * 200), b"A" * 300)]
+    return reads, haps, pairs
+
+
+def main():
+    ref = oracle_lib.ref_phmm()
+    if ref is None:
+        raise SystemExit("oracle/_ref/libref_phmm.so missing: run `make -C oracle ref` first")
+    reads, haps, pairs = phmm_inputs()
+    cross = TestcaseArray(reads, haps)
+    extra = TestcaseArray.from_pairs(pairs)
+    outs = []
+    for ta in (cross, extra):
+        n = ta.n
+        res = {}
+        for eng in (256, 512):
+            out = np.zeros(n)
+            rf = np.zeros(n, np.float32)
+            rd = np.zeros(n)
+            ref.ref_phmm_batch(ctypes.addressof(ta.arr), n, out.ctypes.data, rf.ctypes.data,
+                               rd.ctypes.data, eng, 8)
+            res[eng] = (out, rf, rd)
+        for a, b in zip(res[256], res[512]):
+            assert (a.view(np.uint8) == b.view(np.uint8)).all(), "AVX2 and AVX-512 disagree"
+        outs.append(res[256])
+    field = lambda k: [r[k] for r in reads]
+    np.savez_compressed(
+        os.path.join(HERE, "phmm_golden.npz"),
+        read_bases=np.frombuffer(b"".join(field(0)), np.uint8),
+        read_q=np.frombuffer(b"".join(field(1)), np.uint8),
+        read_i=np.frombuffer(b"".join(field(2)), np.uint8),
+        read_d=np.frombuffer(b"".join(field(3)), np.uint8),
+        read_c=np.frombuffer(b"".join(field(4)), np.uint8),
+        read_len=np.array([len(r[0]) for r in reads], np.int32),
+        hap_bases=np.frombuffer(b"".join(haps), np.uint8),
+        hap_len=np.array([len(h) for h in haps], np.int32),
+        cross_final=outs[0][0], cross_raw_f=outs[0][1], cross_raw_d=outs[0][2],
+        pair_read_bases=np.frombuffer(b"".join(p[0][0] for p in pairs), np.uint8),
+        pair_read_q=np.frombuffer(b"".join(p[0][1] for p in pairs), np.uint8),
+        pair_read_i=np.frombuffer(b"".join(p[0][2] for p in pairs), np.uint8),
+        pair_read_d=np.frombuffer(b"".join(p[0][3] for p in pairs), np.uint8),
+        pair_read_c=np.frombuffer(b"".join(p[0][4] for p in pairs), np.uint8),
+        pair_read_len=np.array([len(p[0][0]) for p in pairs], np.int32),
+        pair_hap_bases=np.frombuffer(b"".join(p[1] for p in pairs), np.uint8),
+        pair_hap_len=np.array([len(p[1]) for p in pairs], np.int32),
+        pair_final=outs[1][0], pair_raw_f=outs[1][1], pair_raw_d=outs[1][2],
+    )
+    print("wrote phmm_golden.npz:", cross.n, "cross testcases,", extra.n, "pairs; f64 fallbacks:",
+          int((outs[0][1] < np.float32(1e-28)).sum()), "; KAT", outs[1][0][0])
+
+
+if __name__ == "__main__":
+    main()

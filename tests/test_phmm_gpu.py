@@ -1,0 +1,136 @@
+"""GPU parity: the HIP PairHMM path (libgb.so, csrc/phmm.hip) against the reference golden vectors
+and the oracle -- bit-exact raw f32/f64 probabilities and final log10 likelihoods (host log10);
+the device log10 epilogue within 1 ulp (north_star tolerance for PairHMM log-likelihoods)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, bits
+from genomicsbench_palisade_amd import gen
+from genomicsbench_palisade_amd._tc import TestcaseArray
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def phmm():
+    from genomicsbench_palisade_amd import phmm, set_device
+    set_device(0)
+    phmm.init_pairhmm()
+    return phmm
+
+
+def oracle_run(ta):
+    import oracle_lib
+    o = oracle_lib.oracle()
+    n = ta.n
+    out, rf, rd = np.zeros(n), np.zeros(n, np.float32), np.zeros(n)
+    ud = np.zeros(n, np.int32)
+    o.phmm_oracle_batch(ctypes.addressof(ta.arr), n, out.ctypes.data, rf.ctypes.data, rd.ctypes.data,
+                        ud.ctypes.data, 16)
+    return out, rf, rd, ud
+
+
+def assert_exact(got, expect):
+    g_out, g_rf, g_rd = got[:3]
+    e_out, e_rf, e_rd = expect[:3]
+    bad = np.nonzero(bits(g_rf) != bits(e_rf))[0]
+    assert len(bad) == 0, f"raw f32 mismatch at {bad[:10]}: {g_rf[bad[:5]]} vs {e_rf[bad[:5]]}"
+    bad = np.nonzero(bits(g_rd) != bits(e_rd))[0]
+    assert len(bad) == 0, f"raw f64 mismatch at {bad[:10]}: {g_rd[bad[:5]]} vs {e_rd[bad[:5]]}"
+    assert (bits(g_out) == bits(e_out)).all()
+
+
+@pytest.mark.parametrize("which", ["cross", "pairs"])
+def test_golden_bit_exact(phmm, phmm_golden, which):
+    got = phmm.compute_likelihoods_both(phmm_golden[which])
+    assert_exact(got, phmm_golden[which + "_expect"])
+
+
+def test_kat(phmm):
+    ta = TestcaseArray.from_pairs([((b"ACGT", b"++++", b"++++", b"++++", b"++++"), b"ACGT")])
+    res = phmm.compute_likelihoods_both(ta)[0]
+    assert res[0] == -0.6022796630859375
+
+
+@pytest.mark.parametrize("seed,kind", [(1, "large"), (2, "small"), (3, "long")])
+def test_random_vs_oracle(phmm, seed, kind):
+    rng = np.random.default_rng(seed)
+    if kind == "large":
+        b = gen.phmm_batch(rng, 64, 32)
+    elif kind == "small":
+        b = gen.phmm_batch(rng, 40, 20, hap_max=302)
+    else:  # long haplotypes / reads beyond the benchmark shapes
+        b = gen.phmm_batch(rng, 6, 5, read_len=(300, 700), hap_max=2000)
+    ta = TestcaseArray.from_batch(b)
+    assert_exact(phmm.compute_likelihoods_both(ta), oracle_run(ta))
+
+
+def test_device_epilogue_within_1ulp(phmm):
+    rng = np.random.default_rng(7)
+    ta = TestcaseArray.from_batch(gen.phmm_batch(rng, 50, 20))
+    db = phmm.DeviceBatch(ta)
+    db.run()
+    res, rf, rd, ud, dev = db.results()
+    # 1 ulp of float at the result's magnitude (north_star: "within 1 ulp float")
+    ulp = np.spacing(np.abs(res).astype(np.float32)).astype(np.float64)
+    assert (np.abs(dev - res) <= ulp).all()
+    t, cells, nf64 = db.stats()
+    assert t == ta.n and nf64 == int(ud.sum())
+    db.close()
+
+
+def test_repeat_runs_identical(phmm):
+    rng = np.random.default_rng(11)
+    ta = TestcaseArray.from_batch(gen.phmm_batch(rng, 30, 30))
+    db = phmm.DeviceBatch(ta)
+    db.run()
+    a = db.results()
+    db.run()
+    db.run()
+    b = db.results()
+    for x, y in zip(a, b):
+        assert (x == y).all()
+    db.close()
+
+
+def test_compute_f64_all(phmm, phmm_golden):
+    import oracle_lib
+    ta = phmm_golden["pairs"]
+    rd = phmm.compute_f64(ta)
+    o = oracle_lib.oracle()
+    exp = np.array([o.phmm_oracle_prob_f64(ctypes.addressof(ta.arr[k])) for k in range(ta.n)])
+    assert (bits(rd) == bits(exp)).all()
+
+
+def test_dropin_symbols(phmm_golden):
+    """libgkl_pairhmm_c.so exports the reference's C++ entry points; call them via their mangled
+    names exactly as a binary linked against GKL would."""
+    so = ctypes.CDLL(os.path.join(ROOT, "genomicsbench_palisade_amd", "lib", "libgkl_pairhmm_c.so"))
+    so._Z11initPairHMMv()
+    ta = phmm_golden["cross"]
+    out = np.zeros(ta.n)
+    so._Z22computelikelihoodsbothP8testcasePdi(ctypes.addressof(ta.arr), out.ctypes.data, ta.n)
+    assert (bits(out) == bits(phmm_golden["cross_expect"][0])).all()
+
+
+def test_phmm_cli(tmp_path):
+    """bin/phmm parses the reference's .in format and prints PRINT_OUTPUT lines."""
+    rng = np.random.default_rng(5)
+    batches = [gen.phmm_batch(rng, 5, 3), gen.phmm_batch(rng, 7, 4, hap_max=302)]
+    path = tmp_path / "t.in"
+    gen.write_phmm_file(str(path), batches)
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "phmm")
+    out = subprocess.run([exe, "-f", str(path), "-p"], capture_output=True, text=True, timeout=300,
+                         check=True).stdout
+    vals = [float(x) for x in out.split("Num GPUs")[1].splitlines()[1:] if x.strip() and "PairHMM" not in x]
+    expect = []
+    for b in batches:
+        ta = TestcaseArray.from_batch(b)
+        expect.extend(oracle_run(ta)[0])
+    assert len(vals) == len(expect)
+    assert np.allclose(vals, expect, atol=1e-6, rtol=0)  # "%lf" prints 6 decimals
+    assert "PairHMM completed. Kernel runtime:" in out
