@@ -170,10 +170,10 @@ __device__ __forceinline__ float select_dist(uint32_t rmask, uint32_t h, float d
   uint32_t r = (m & __builtin_bit_cast(uint32_t, dmatch)) | (~m & __builtin_bit_cast(uint32_t, dmis));
   return __builtin_bit_cast(float, r);
 }
+// (f64: a plain select -- hipcc 7.2 mis-derives the high word of a sign-extended sbfe mask and
+// constant-folds it, so the 64-bit bit-insert form is not used.)
 __device__ __forceinline__ double select_dist(uint32_t rmask, uint32_t h, double dmatch, double dmis) {
-  uint64_t m = (uint64_t)(int64_t)__builtin_amdgcn_sbfe((int)rmask, h, 1);
-  uint64_t r = (m & __builtin_bit_cast(uint64_t, dmatch)) | (~m & __builtin_bit_cast(uint64_t, dmis));
-  return __builtin_bit_cast(double, r);
+  return ((rmask >> h) & 1u) ? dmatch : dmis;
 }
 
 // One testcase per 64-lane workgroup. `list`/`list_count` (f64 pass) remap blockIdx to the
