@@ -9,7 +9,7 @@ CSRC := $(PKG)/csrc
 LIB := $(PKG)/lib
 BIN := $(PKG)/bin
 # -ffp-contract=off is part of the arithmetic contract (no FMA anywhere).
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-result
 HOSTCXX := g++
 HOSTFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off -Wall
 

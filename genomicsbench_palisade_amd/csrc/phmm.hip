@@ -34,6 +34,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kMaxHaplen = 4096;
+constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_stripe reads)
 constexpr int kQualTab = 128;
 constexpr int kM2M = ((127 * 128) >> 1) + 128;  // set_mm_prob indices for quals < 128
 
@@ -131,36 +132,40 @@ struct DevTab {
   T init_const;
 };
 
-// Boundary record per column: the row above the stripe (written by lane 63 of the previous
-// stripe) plus the haplotype base code of that column, read by lane 0 with one uniform LDS load.
+// Boundary record per column c (stripe above the current one): the two partial sums the first
+// row of the current stripe needs from the row above, already multiplied by THAT first row's
+// transition probabilities, plus the haplotype base code of column c:
+//   z = (M*pMM + X*pGAPM) + Y*pGAPM   (the M recurrence's bracket, used one column later)
+//   w = M*pMX + X*pXX                 (= X of the next row at the same column)
+// Read by lane 0 with one uniform ds_read per step. The haplotype codes live in a separate byte
+// array that every lane reads at its own column (no cross-lane traffic, no VALU).
 template <typename T>
-struct Brec;
-template <>
-struct __attribute__((aligned(16))) Brec<float> {
-  float m, x, y;
-  uint32_t h;
-};
-template <>
-struct __attribute__((aligned(16))) Brec<double> {
-  double m, x, y;
-  uint64_t h;
+struct __attribute__((aligned(2 * sizeof(T)))) Brec {
+  T z, w;
 };
 
 __device__ __forceinline__ int dpp_shr(int v, int lane0) {
   // wave_shr:1 (DPP ctrl 0x138); lane 0 has no source lane and keeps `lane0` (bound_ctrl off).
   return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);
 }
-__device__ __forceinline__ float shr(float v, float lane0) {
-  return __builtin_bit_cast(float, dpp_shr(__builtin_bit_cast(int, v), __builtin_bit_cast(int, lane0)));
+__device__ __forceinline__ int dpp_shl(int v, int lane63) {
+  // wave_shl:1 (DPP ctrl 0x130); lane 63 has no source lane and keeps `lane63`.
+  return __builtin_amdgcn_update_dpp(lane63, v, 0x130, 0xF, 0xF, false);
 }
-__device__ __forceinline__ double shr(double v, double lane0) {
-  long long vb = __builtin_bit_cast(long long, v), lb = __builtin_bit_cast(long long, lane0);
-  int lo = dpp_shr((int)(vb & 0xffffffffll), (int)(lb & 0xffffffffll));
-  int hi = dpp_shr((int)(vb >> 32), (int)(lb >> 32));
+template <int (*F)(int, int)>
+__device__ __forceinline__ float dpp(float v, float keep) {
+  return __builtin_bit_cast(float, F(__builtin_bit_cast(int, v), __builtin_bit_cast(int, keep)));
+}
+template <int (*F)(int, int)>
+__device__ __forceinline__ double dpp(double v, double keep) {
+  long long vb = __builtin_bit_cast(long long, v), kb = __builtin_bit_cast(long long, keep);
+  int lo = F((int)(vb & 0xffffffffll), (int)(kb & 0xffffffffll));
+  int hi = F((int)(vb >> 32), (int)(kb >> 32));
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ uint32_t shr(uint32_t v, uint32_t lane0) {
-  return (uint32_t)dpp_shr((int)v, (int)lane0);
+template <int (*F)(int, int)>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t keep) {
+  return (uint32_t)F((int)v, (int)keep);
 }
 
 // dist select without a compare: sign-extend bit `h` of the lane's match mask (0 or ~0) and
@@ -176,8 +181,110 @@ __device__ __forceinline__ double select_dist(uint32_t rmask, uint32_t h, double
   return ((rmask >> h) & 1u) ? dmatch : dmis;
 }
 
-// One testcase per 64-lane workgroup. `list`/`list_count` (f64 pass) remap blockIdx to the
-// testcases the f32 pass flagged.
+// Per-lane constants of one stripe (initializeVectors, avx-pairhmm-template.h:83-128): the lane's
+// own row (Y recurrence, emission) and the NEXT row's transitions (the partials z/w it hands down).
+template <typename T>
+struct RowParams {
+  T pMY, pYY, dmatch, dmis;              // own row
+  T nMM, nGAPM, nMX, nXX;                // row below (lane+1; lane 63: first row of next stripe)
+  uint32_t rmask;
+};
+
+// Lane state between steps. Row r = lane's row, column c = step - lane + 1:
+//   Mp, Yp : M[r][c-1], Y[r][c-1]           zo, wo : this lane's z/w of column c-1
+//   zd     : z of row r-1 at column c-1 (= the M bracket of this lane's next cell), shifted in
+template <typename T>
+struct LaneState {
+  T Mp, Yp, zo, wo, zd;
+  T cz, cw;  // collectors: lane j holds lane 63's z/w of 63-j steps ago (stripe boundary writer)
+};
+
+// One anti-diagonal step. Arithmetic per cell is exactly the reference's (no FMA, same order):
+//   X = M[r-1][c]*pMX + X[r-1][c]*pXX         computed by lane-1 as w, shifted in
+//   M = ((M*pMM + X*pGAPM) + Y*pGAPM)[r-1][c-1] * dist    bracket computed by lane-1 as z
+//   Y = M[r][c-1]*pMY + Y[r][c-1]*pYY
+template <typename T, bool kLast>
+__device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneState<T> &st,
+                                          const RowParams<T> &P, T &sumM, T &sumX) {
+  const T X = dpp<dpp_shr>(st.wo, rec.w);          // X[r][c]
+  const T zdn = dpp<dpp_shr>(st.zo, rec.z);        // bracket for column c+1
+  const T dist = select_dist(P.rmask, h, P.dmatch, P.dmis);
+  const T M = st.zd * dist;
+  const T Y = st.Mp * P.pMY + st.Yp * P.pYY;
+  st.zo = (M * P.nMM + X * P.nGAPM) + Y * P.nGAPM;
+  st.wo = M * P.nMX + X * P.nXX;
+  if constexpr (kLast) {
+    sumM = sumM + M;
+    sumX = sumX + X;
+  } else {
+    st.cz = dpp<dpp_shl>(st.cz, st.zo);
+    st.cw = dpp<dpp_shl>(st.cw, st.wo);
+  }
+  st.zd = zdn;
+  st.Mp = M;
+  st.Yp = Y;
+}
+
+// Lane j of the collectors holds lane 63's z/w of step t-63+j, i.e. column t-125+j of the row
+// below this stripe; write the ones that are real columns.
+template <typename T>
+__device__ __forceinline__ void flush_boundary(const LaneState<T> &st, Brec<T> *__restrict__ bnd, int t,
+                                               int C, int lane) {
+  const int c = t - 125 + lane;
+  if (c >= 1 && c <= C) {
+    bnd[c].z = st.cz;
+    bnd[c].w = st.cw;
+  }
+}
+
+// Sweep `steps` anti-diagonals of one stripe, 4 per iteration, the boundary records of the next
+// block prefetched before this block runs (reads are at columns > t, boundary writes at <= t-62).
+template <typename T, bool kLast>
+__device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const RowParams<T> &P,
+                                            T &sumM, T &sumX, Brec<T> *__restrict__ bnd,
+                                            const uint8_t *__restrict__ hcol, int C, int lane) {
+  // hcol[c] = haplotype code of column c (valid for c in [-63, C+kBndPad)); lane's column at step
+  // t is t - lane + 1.
+  const uint8_t *hl = hcol + 1 - lane;
+  constexpr int U = 4;
+  int t = 0;
+  for (; t + U <= steps; t += U) {
+    // records land directly in the DPP "old" registers (no rotation copies); the LDS latency is
+    // covered by the other waves on the SIMD
+    const Brec<T> c0 = bnd[t + 1], c1 = bnd[t + 2], c2 = bnd[t + 3], c3 = bnd[t + 4];
+    const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
+    phmm_step<T, kLast>(c0, h0, st, P, sumM, sumX);
+    phmm_step<T, kLast>(c1, h1, st, P, sumM, sumX);
+    phmm_step<T, kLast>(c2, h2, st, P, sumM, sumX);
+    phmm_step<T, kLast>(c3, h3, st, P, sumM, sumX);
+    if constexpr (!kLast) {
+      if (((t + U) & (kWave - 1)) == 0) flush_boundary(st, bnd, t + U - 1, C, lane);
+    }
+  }
+  for (; t < steps; t++) phmm_step<T, kLast>(bnd[t + 1], hl[t], st, P, sumM, sumX);
+  if constexpr (!kLast) flush_boundary(st, bnd, steps - 1, C, lane);
+}
+
+template <typename T>
+__device__ __forceinline__ void load_row(const uint8_t *__restrict__ rbase, int R, int row,
+                                         const DevTab<T> &tab, T &pMM, T &pGAPM, T &pMX, T &pXX,
+                                         T &pMY, T &pYY, T &dmatch, T &dmis, uint32_t &rmask) {
+  rmask = rbase[row];
+  const int q = rbase[R + row] & 127, qi = rbase[2 * R + row] & 127;
+  const int qd = rbase[3 * R + row] & 127, qc = rbase[4 * R + row] & 127;
+  const int mn = qi <= qd ? qi : qd, mx = qi <= qd ? qd : qi;
+  pMM = tab.m2m[((mx * (mx + 1)) >> 1) + mn];
+  pGAPM = tab.one_minus[qc];
+  pMX = tab.ph2pr[qi];
+  pXX = tab.ph2pr[qc];
+  pMY = tab.ph2pr[qd];
+  pYY = tab.ph2pr[qc];
+  dmatch = tab.one_minus[q];
+  dmis = tab.div3[q];
+}
+
+// One testcase per 64-lane workgroup. f64 pass: `f64_list`/`f64_count` remap blockIdx to the
+// testcases the f32 pass flagged (null list = every testcase).
 template <typename T, bool kF64Pass>
 __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ descs,
                                                     const uint8_t *__restrict__ pool,
@@ -185,11 +292,10 @@ __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ de
                                                     int *__restrict__ f64_list,
                                                     int *__restrict__ f64_count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw);
 
   int w = blockIdx.x;
   if constexpr (kF64Pass) {
-    if (f64_count) {  // null list = f64 for every testcase (computelikelihoodsdouble)
+    if (f64_count) {
       if (w >= *f64_count) return;
       w = f64_list[w];
     }
@@ -199,73 +305,60 @@ __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ de
   const int C = (int)(desc.dims >> 16);
   const int lane = threadIdx.x;
   const T init_Y = tab.init_const / (T)C;
+  const uint8_t *rbase = pool + desc.read_off;
+  // LDS: boundary records for columns [0, C+kBndPad), then haplotype codes for columns
+  // [-kWave, C+kBndPad) (codes 0 outside 1..C; cells outside the matrix never feed real cells).
+  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw);
+  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad) + kWave;
 
-  // boundary row 0 (M = X = 0, Y = init_Y) and the haplotype codes, columns 0 .. C+64
+  // Row 0 -> first row's partials: M = X = 0, Y = init_Y, so z = (0*pMM + 0*pGAPM) + init_Y*pGAPM
+  // (evaluated, not simplified, to keep the reference's operation order) and w = 0*pMX + 0*pXX.
+  T z0, w0;
+  {
+    T pMM, pGAPM, pMX, pXX, pMY, pYY, dm, dx;
+    uint32_t rm;
+    load_row(rbase, R, 0, tab, pMM, pGAPM, pMX, pXX, pMY, pYY, dm, dx, rm);
+    const T zero = (T)0;
+    z0 = (zero * pMM + zero * pGAPM) + init_Y * pGAPM;
+    w0 = zero * pMX + zero * pXX;
+  }
   const uint8_t *hcode = pool + desc.hap_off;
-  for (int c = lane; c <= C + kWave; c += kWave) {
+  for (int c = lane; c < C + kBndPad; c += kWave) {
     Brec<T> b;
-    b.m = (T)0;
-    b.x = (T)0;
-    b.y = init_Y;
-    b.h = (c >= 1 && c <= C) ? hcode[c - 1] : 0;
+    b.z = z0;
+    b.w = w0;
     bnd[c] = b;
   }
+  for (int c = lane - kWave; c < C + kBndPad; c += kWave) hcol[c] = (c >= 1 && c <= C) ? hcode[c - 1] : 0;
   __syncthreads();
 
-  const uint8_t *rbase = pool + desc.read_off;
   const int nstripes = (R + kWave - 1) / kWave;
   T result = (T)0;
   for (int s = 0; s < nstripes; s++) {
     const int r0 = s * kWave;
     const int nrows = min(kWave, R - r0);
-    const bool last = (s == nstripes - 1);
-    const int row = min(r0 + lane, R - 1);
-    const uint32_t rmask = rbase[row];
-    const int q = rbase[R + row] & 127, qi = rbase[2 * R + row] & 127;
-    const int qd = rbase[3 * R + row] & 127, qc = rbase[4 * R + row] & 127;
-    const int mn = qi <= qd ? qi : qd, mx = qi <= qd ? qd : qi;
-    const T pMM = tab.m2m[((mx * (mx + 1)) >> 1) + mn];
-    const T pGAPM = tab.one_minus[qc];
-    const T pMX = tab.ph2pr[qi], pXX = tab.ph2pr[qc];
-    const T pMY = tab.ph2pr[qd], pYY = tab.ph2pr[qc];
-    const T dmatch = tab.one_minus[q], dmis = tab.div3[q];
-
-    T Mp = 0, Xp = 0, Yp = 0;  // (r, c-1)
-    T dM = 0, dX = 0, dY = (s == 0 && lane == 0) ? init_Y : (T)0;  // (r-1, c-1)
-    uint32_t h = 0;
-    T sumM = 0, sumX = 0;
-    const int steps = last ? C + nrows - 1 : C + kWave - 1;
-    Brec<T> nxt = bnd[1];
-    for (int t = 0; t < steps; t++) {
-      const Brec<T> cur = nxt;
-      nxt = bnd[t + 2];  // prefetch: index t+2 never aliases this step's write (t-62)
-      const T uM = shr(Mp, cur.m);
-      const T uX = shr(Xp, cur.x);
-      const T uY = shr(Yp, cur.y);
-      h = shr(h, (uint32_t)cur.h);
-      const T dist = select_dist(rmask, h, dmatch, dmis);
-      const T M = ((dM * pMM + dX * pGAPM) + dY * pGAPM) * dist;
-      const T X = uM * pMX + uX * pXX;
-      const T Y = Mp * pMY + Yp * pYY;
-      if (last) {
-        sumM = sumM + M;
-        sumX = sumX + X;
-      } else if (lane == kWave - 1) {
-        const int c = t - (kWave - 2);
-        if (c >= 1) {
-          bnd[c].m = M;
-          bnd[c].x = X;
-          bnd[c].y = Y;
-        }
-      }
-      dM = uM;
-      dX = uX;
-      dY = uY;
-      Mp = M;
-      Xp = X;
-      Yp = Y;
+    RowParams<T> P;
+    {
+      T pMM, pGAPM, pMX, pXX;
+      load_row(rbase, R, min(r0 + lane, R - 1), tab, pMM, pGAPM, pMX, pXX, P.pMY, P.pYY, P.dmatch,
+               P.dmis, P.rmask);
+      T a, b, d, e;
+      uint32_t f;
+      load_row(rbase, R, min(r0 + lane + 1, R - 1), tab, P.nMM, P.nGAPM, P.nMX, P.nXX, a, b, d, e, f);
     }
-    if (last) result = sumM + sumX;
+    LaneState<T> st;
+    st.Mp = st.Yp = st.zo = st.wo = (T)0;
+    st.zd = (lane == 0) ? bnd[0].z : (T)0;  // bracket at column 0: z0 for stripe 0, 0 below
+    st.cz = st.cw = (T)0;
+    T sumM = (T)0, sumX = (T)0;
+    if (s == nstripes - 1) {
+      phmm_stripe<T, true>(C + nrows - 1, st, P, sumM, sumX, bnd, hcol, C, lane);
+      result = sumM + sumX;
+    } else {
+      phmm_stripe<T, false>(C + kWave - 1, st, P, sumM, sumX, bnd, hcol, C, lane);
+      if (lane == 0) bnd[0].z = (T)0;  // rows >= 1 have M = X = Y = 0 at column 0
+    }
+    __syncthreads();
   }
   if (lane == ((R - 1) & (kWave - 1))) {
     raw_out[desc.out_idx] = result;
@@ -529,8 +622,8 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipMemsetAsync(b->d_count, 0, sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
-    const size_t lds_f = sizeof(Brec<float>) * (size_t)(b->max_haplen + kWave + 2);
-    const size_t lds_d = sizeof(Brec<double>) * (size_t)(b->max_haplen + kWave + 2);
+    const size_t lds_f = (sizeof(Brec<float>) + 1) * (size_t)(b->max_haplen + kBndPad) + kWave + 16;
+    const size_t lds_d = (sizeof(Brec<double>) + 1) * (size_t)(b->max_haplen + kBndPad) + kWave + 16;
     if (!b->force_f64) {
       hipLaunchKernelGGL((phmm_forward<float, false>), dim3(n), dim3(kWave), lds_f, b->stream,
                          b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,
