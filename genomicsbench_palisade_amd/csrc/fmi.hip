@@ -1,0 +1,715 @@
+// fmi.hip -- MI355X (gfx950) bwa-mem2 SMEM search: index upload, search kernel, compaction, C ABI.
+//
+// Semantics (the reference's plaintext arithmetic; HE layer is an identity):
+//   backwardExt           tools/bwa-mem2/src/FMI_search.cpp:1536-1565 (Occ = GET_OCC, FMI_search.h:81-89)
+//   SMEMs at one position FMI_search.cpp:986-1180   (getSMEMsOnePosOneThread)
+//   all positions         FMI_search.cpp:1182-1241  (getSMEMsAllPosOneThread)
+//   LAST seeds            FMI_search.cpp:1243-1326  (bwtSeedStrategyAllPosOneThread)
+//   batch pipeline        benchmarks/fmi/fmi.cpp:253-348 (smem1, reseed, LAST, rid offset, sort)
+//
+// MI355X design: the work is a chain of dependent random 64-byte gathers (two CP_OCC lines per
+// backwardExt) with data-dependent control flow. One read per lane, and every lane runs a state
+// machine that issues exactly one backwardExt per loop trip, so the divergent bookkeeping between
+// extensions is short and the gathers of all 64 lanes issue together; thousands of waves keep the
+// HBM/Infinity-Cache latency covered. A lane that finishes a read takes the next one from a
+// device-wide counter (per-wave aggregated atomic), so long and short reads balance. Each lane's
+// `prev` list lives in a private scratch slice (L2-resident in practice); each read's SMEMs go to a
+// fixed-capacity slot, are insertion-sorted by (m asc, n desc) in place, then compacted by an
+// exclusive scan + scatter into the reference's (rid, m, n desc) order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gb_fmi.h"
+#include "../../include/gb.h"
+#include "gb_common.h"
+#include "fmi_index.h"
+
+namespace gbfmi {
+
+constexpr int kCap = 64;  // SMEM slots per read (7.7 on average on the synthetic sets; overflow is an error)
+
+struct __attribute__((aligned(16))) Ent {  // one `prev` entry (SMEM without rid)
+  int64_t k, l, s;
+  uint32_t m, n;
+};
+
+struct DevIndex {
+  const CpOcc *occ;
+  int64_t count[5];
+  int64_t sentinel;
+};
+
+__device__ __forceinline__ uint64_t occ_mask(int y) { return y ? (~0ull << (64 - y)) : 0ull; }
+
+// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). Both CP_OCC lines are
+// loaded whole (64 B each); when sp and ep share a line the second load is skipped.
+__device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l, int64_t s, int a,
+                                        int64_t &ko, int64_t &lo, int64_t &so) {
+  const int64_t sp = k, ep = k + s;
+  const int64_t bs = sp >> 6, be = ep >> 6;
+  const CpOcc A = F.occ[bs];
+  CpOcc B;
+  if (be != bs)
+    B = F.occ[be];
+  else
+    B = A;
+  const uint64_t ms = occ_mask((int)(sp & 63)), me = occ_mask((int)(ep & 63));
+  int64_t os[4], oe[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    os[b] = A.cp_count[b] + __popcll(A.one_hot_bwt_str[b] & ms);
+    oe[b] = B.cp_count[b] + __popcll(B.one_hot_bwt_str[b] & me);
+  }
+  const int64_t off = (k <= F.sentinel && k + s > F.sentinel) ? 1 : 0;
+  const int64_t s3 = oe[3] - os[3], s2 = oe[2] - os[2], s1 = oe[1] - os[1], s0 = oe[0] - os[0];
+  const int64_t l3 = l + off, l2 = l3 + s3, l1 = l2 + s2, l0 = l1 + s1;
+  switch (a) {
+    case 0: ko = F.count[0] + os[0]; so = s0; lo = l0; break;
+    case 1: ko = F.count[1] + os[1]; so = s1; lo = l1; break;
+    case 2: ko = F.count[2] + os[2]; so = s2; lo = l2; break;
+    default: ko = F.count[3] + os[3]; so = s3; lo = l3; break;
+  }
+}
+
+enum State : int {
+  NEXT_READ,
+  OP_START,   // getSMEMsOnePosOneThread at x
+  FWD_NEXT,   // forward extension loop
+  FWD_END,
+  BWD_ITER,   // backward search, one j
+  BWD_P,      // ... one prev entry
+  BWD_FINAL,
+  OP_END,
+  P2_NEXT,    // reseeding over this read's phase-1 SMEMs
+  P3_X,       // LAST seeds
+  P3_NEXT,
+  FINISH,
+  DONE,
+};
+
+struct SearchArgs {
+  DevIndex F;
+  const uint8_t *qdb;
+  const int32_t *lens;
+  int32_t nreads, stride, min_seed_len, split_len;
+  Ent *scratch;          // per lane: stride entries
+  gb_smem *slots;        // per read: kCap entries
+  int32_t *counts;       // per read: total SMEMs
+  int32_t *phase;        // per read: num_smem1, num_smem2, num_smem3
+  int32_t *next_read;    // work counter
+  int32_t *overflow;     // reads that exceeded kCap
+  unsigned long long *bwt_calls;
+};
+
+__device__ __forceinline__ bool smem_less(const gb_smem &a, const gb_smem &b) {
+  return a.m < b.m || (a.m == b.m && a.n > b.n);  // compare_smem, FMI_search.cpp:1499-1518
+}
+
+__global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
+  const DevIndex F = A.F;
+  const int gid = blockIdx.x * 64 + threadIdx.x;
+  Ent *const prev = A.scratch + (size_t)gid * A.stride;
+  unsigned long long calls = 0;
+
+  int st = NEXT_READ;
+  int rd = 0, L = 0, mode = 0;
+  const uint8_t *q = nullptr;
+  gb_smem *o = nullptr;
+  int nout = 0, n1 = 0, n2 = 0, ridx = 0;
+  bool ovf = false;
+  int x = 0, min_intv = 1, j = 0, next_x = 0, numPrev = 0, numCurr = 0, p = 0, curr_s = -1, a = 0;
+  bool first = true;
+  int64_t ck = 0, cl = 0, cs = 0;  // current SMEM of a forward extension
+  uint32_t cm = 0;
+  Ent *r = prev;                   // reversed prev list: r[0] = last pushed
+
+  auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
+    if (nout < kCap) {
+      gb_smem e;
+      e.rid = (uint32_t)rd;
+      e.m = m;
+      e.n = n;
+      e.k = k;
+      e.l = l;
+      e.s = s;
+      o[nout] = e;
+    } else {
+      ovf = true;
+    }
+    nout++;
+  };
+
+  while (true) {
+    // ---- advance this lane's state machine to its next backwardExt request --------------------
+    int64_t rk = 0, rl = 0, rs = 0;
+    int rb = 0;
+    bool req = false;
+    while (!req && st != DONE) {
+      switch (st) {
+        case NEXT_READ:
+          rd = atomicAdd(A.next_read, 1);
+          if (rd >= A.nreads) {
+            st = DONE;
+            break;
+          }
+          L = A.lens[rd];
+          q = A.qdb + (size_t)rd * A.stride;
+          o = A.slots + (size_t)rd * kCap;
+          nout = 0;
+          ovf = false;
+          mode = 1;
+          x = 0;
+          min_intv = 1;
+          st = OP_START;
+          break;
+        case OP_START:
+          if (mode == 1 && x >= L) {  // getSMEMsAllPosOneThread done: reseed next
+            n1 = nout;
+            ridx = 0;
+            mode = 2;
+            st = P2_NEXT;
+            break;
+          }
+          next_x = x + 1;
+          a = q[x];
+          if (a >= 4) {
+            st = OP_END;
+            break;
+          }
+          ck = F.count[a];
+          cl = F.count[3 - a];
+          cs = F.count[a + 1] - F.count[a];
+          cm = (uint32_t)x;
+          numPrev = 0;
+          j = x + 1;
+          st = FWD_NEXT;
+          break;
+        case FWD_NEXT:
+          if (j >= L) {
+            st = FWD_END;
+            break;
+          }
+          next_x = j + 1;
+          a = q[j];
+          if (a >= 4) {
+            st = FWD_END;
+            break;
+          }
+          // forward extension = backward extension on the reverse complement (k <-> l, 3 - a)
+          rk = cl;
+          rl = ck;
+          rs = cs;
+          rb = 3 - a;
+          req = true;
+          break;
+        case FWD_END:
+          if (cs >= min_intv) {
+            Ent e;
+            e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);  // current n = j-1
+            prev[L - 1 - numPrev] = e;
+            numPrev++;
+          }
+          r = prev + (L - numPrev);
+          j = x - 1;
+          st = BWD_ITER;
+          break;
+        case BWD_ITER:
+          if (j < 0) {
+            st = BWD_FINAL;
+            break;
+          }
+          a = q[j];
+          if (a > 3) {
+            st = BWD_FINAL;
+            break;
+          }
+          numCurr = 0;
+          curr_s = -1;
+          first = true;
+          p = 0;
+          st = BWD_P;
+          break;
+        case BWD_P:
+          if (p >= numPrev) {
+            numPrev = numCurr;
+            if (numCurr == 0) {
+              st = OP_END;
+            } else {
+              j--;
+              st = BWD_ITER;
+            }
+            break;
+          }
+          {
+            const Ent e = r[p];
+            rk = e.k;
+            rl = e.l;
+            rs = e.s;
+            rb = a;
+            req = true;
+          }
+          break;
+        case BWD_FINAL:
+          if (numPrev != 0) {
+            const Ent e = r[0];
+            if ((e.n - e.m + 1) >= (uint32_t)A.min_seed_len) emit(e.k, e.l, e.s, e.m, e.n);
+          }
+          st = OP_END;
+          break;
+        case OP_END:
+          if (mode == 1) {
+            x = next_x;
+            st = OP_START;
+          } else {
+            ridx++;
+            st = P2_NEXT;
+          }
+          break;
+        case P2_NEXT: {
+          // fmi.cpp:293-302: SMEMs of length >= split_len with s <= splitWidth(10) restart at
+          // the midpoint with min_intv = s + 1
+          bool found = false;
+          while (ridx < n1 && ridx < kCap) {
+            const gb_smem e = o[ridx];
+            const int start = (int)e.m, end = (int)e.n + 1;
+            if (!(end - start < A.split_len || e.s > 10)) {
+              x = (end + start) >> 1;
+              min_intv = (int)(e.s + 1);
+              found = true;
+              break;
+            }
+            ridx++;
+          }
+          if (found) {
+            st = OP_START;
+          } else {
+            n2 = nout - n1;
+            mode = 3;
+            x = 0;
+            st = P3_X;
+          }
+          break;
+        }
+        case P3_X:
+          if (x >= L) {
+            st = FINISH;
+            break;
+          }
+          next_x = x + 1;
+          a = q[x];
+          if (a >= 4) {
+            x = next_x;
+            break;
+          }
+          ck = F.count[a];
+          cl = F.count[3 - a];
+          cs = F.count[a + 1] - F.count[a];
+          cm = (uint32_t)x;
+          j = x + 1;
+          st = P3_NEXT;
+          break;
+        case P3_NEXT:
+          if (j >= L) {
+            x = next_x;
+            st = P3_X;
+            break;
+          }
+          next_x = j + 1;
+          a = q[j];
+          if (a >= 4) {
+            x = next_x;
+            st = P3_X;
+            break;
+          }
+          rk = cl;
+          rl = ck;
+          rs = cs;
+          rb = 3 - a;
+          req = true;
+          break;
+        case FINISH: {
+          const int n = nout < kCap ? nout : kCap;
+          for (int i = 1; i < n; i++) {  // insertion sort by (m asc, n desc)
+            const gb_smem e = o[i];
+            int t = i - 1;
+            while (t >= 0 && smem_less(e, o[t])) {
+              o[t + 1] = o[t];
+              t--;
+            }
+            o[t + 1] = e;
+          }
+          A.counts[rd] = n;
+          A.phase[3 * rd + 0] = n1;
+          A.phase[3 * rd + 1] = n2;
+          A.phase[3 * rd + 2] = nout - n1 - n2;
+          if (ovf) atomicAdd(A.overflow, 1);
+          st = NEXT_READ;
+          break;
+        }
+        default:
+          st = DONE;
+          break;
+      }
+    }
+    if (st == DONE) break;
+
+    // ---- one backwardExt per lane per trip --------------------------------------------------
+    int64_t ko, lo, so;
+    bwt_ext(F, rk, rl, rs, rb, ko, lo, so);
+    calls++;
+
+    // ---- consume ------------------------------------------------------------------------------
+    if (st == FWD_NEXT) {
+      // newSmem = swap(result); n = j (FMI_search.cpp:1044-1056)
+      const int64_t nk = lo, nl = ko, ns = so;
+      if (ns != cs) {  // push the current SMEM (prevArray[numPrev] = smem; numPrev += s_neq)
+        Ent e;
+        e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);
+        prev[L - 1 - numPrev] = e;
+        numPrev++;
+      }
+      if (ns < min_intv) {
+        next_x = j;
+        st = FWD_END;
+      } else {
+        ck = nk;
+        cl = nl;
+        cs = ns;
+        j++;
+      }
+    } else if (st == BWD_P) {
+      const Ent e = r[p];
+      if (first) {
+        if (so < min_intv && (e.n - e.m + 1) >= (uint32_t)A.min_seed_len) {
+          emit(e.k, e.l, e.s, e.m, e.n);
+          first = false;
+        } else if (so >= min_intv && so != (int64_t)curr_s) {
+          curr_s = (int)so;
+          Ent ne;
+          ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
+          r[numCurr++] = ne;
+          first = false;
+        }
+      } else if (so >= min_intv && so != (int64_t)curr_s) {
+        curr_s = (int)so;
+        Ent ne;
+        ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
+        r[numCurr++] = ne;
+      }
+      p++;
+    } else {  // P3_NEXT (bwtSeedStrategyAllPosOneThread)
+      ck = lo;
+      cl = ko;
+      cs = so;
+      if (cs < 20 && (uint32_t)(j - (int)cm + 1) >= (uint32_t)(A.min_seed_len + 1)) {
+        if (cs > 0) emit(ck, cl, cs, cm, (uint32_t)j);
+        x = j + 1;
+        st = P3_X;
+      } else {
+        j++;
+      }
+    }
+  }
+  atomicAdd(A.bwt_calls, calls);
+}
+
+__global__ void scatter_smems(const gb_smem *__restrict__ slots, const int32_t *__restrict__ counts,
+                              const int64_t *__restrict__ offsets, gb_smem *__restrict__ out,
+                              int32_t nreads) {
+  const int rd = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rd >= nreads) return;
+  const int n = counts[rd];
+  const int64_t o = offsets[rd];
+  for (int i = 0; i < n; i++) out[o + i] = slots[(size_t)rd * kCap + i];
+}
+
+}  // namespace gbfmi
+
+// ---------------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------------
+struct gb_fmi_reads {
+  gb_fmi_index *idx = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  int32_t nreads = 0, stride = 0;
+  int lanes = 0;
+  uint8_t *d_qdb = nullptr;
+  int32_t *d_lens = nullptr;
+  gbfmi::Ent *d_scratch = nullptr;
+  gb_smem *d_slots = nullptr;
+  int32_t *d_counts = nullptr;
+  int32_t *d_phase = nullptr;
+  int64_t *d_offsets = nullptr;
+  gb_smem *d_out = nullptr;
+  int64_t out_cap = 0;
+  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow
+  unsigned long long *d_calls = nullptr;
+  void *d_temp = nullptr;
+  size_t temp_bytes = 0;
+  bool ran = false;
+};
+
+namespace {
+
+int lanes_for_device() {
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  const char *e = getenv("GB_FMI_WAVES_PER_CU");
+  const int waves = e ? std::max(1, atoi(e)) : 16;
+  return cus * waves * 64;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gb_fmi_index_load(const char *path, gb_fmi_index **out) {
+  GB_ARG(path && out, "gb_fmi_index_load: null argument");
+  *out = nullptr;
+  FILE *fp = fopen(path, "rb");
+  if (!fp) {
+    gb::set_error("gb_fmi_index_load: cannot open %s", path);
+    return GB_ERR_ARG;
+  }
+  int64_t n = 0, count[5];
+  if (fread(&n, 8, 1, fp) != 1 || fread(count, 8, 5, fp) != 5 || n <= 1) {
+    fclose(fp);
+    gb::set_error("gb_fmi_index_load: %s: bad header", path);
+    return GB_ERR_ARG;
+  }
+  const int64_t cp_size = (n >> 6) + 1;
+  std::vector<gbfmi::CpOcc> occ((size_t)cp_size);
+  if (fread(occ.data(), sizeof(gbfmi::CpOcc), (size_t)cp_size, fp) != (size_t)cp_size) {
+    fclose(fp);
+    gb::set_error("gb_fmi_index_load: %s: truncated CP_OCC table", path);
+    return GB_ERR_ARG;
+  }
+  const int64_t ns = (n >> 3) + 1;  // SA_COMPRESSION with SA_COMPX = 3 (macro.h:64-66)
+  int64_t sentinel = -1;
+  if (fseek(fp, ns * 5, SEEK_CUR) != 0 || fread(&sentinel, 8, 1, fp) != 1) {
+    fclose(fp);
+    gb::set_error("gb_fmi_index_load: %s: truncated (sampled SA / sentinel)", path);
+    return GB_ERR_ARG;
+  }
+  fclose(fp);
+  auto *idx = new gb_fmi_index();
+  GB_HIP(hipGetDevice(&idx->device));
+  idx->n = n;
+  for (int b = 0; b < 5; b++) idx->count[b] = count[b] + 1;  // FMI_search.cpp:763-768
+  idx->sentinel = sentinel;
+  idx->cp_size = cp_size;
+  hipError_t e = hipMalloc(&idx->d_occ, sizeof(gbfmi::CpOcc) * (size_t)cp_size);
+  if (e == hipSuccess)
+    e = hipMemcpy(idx->d_occ, occ.data(), sizeof(gbfmi::CpOcc) * (size_t)cp_size, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    gb::set_error("gb_fmi_index_load: %s", hipGetErrorString(e));
+    (void)hipFree(idx->d_occ);
+    delete idx;
+    return GB_ERR_HIP;
+  }
+  *out = idx;
+  return GB_OK;
+}
+
+int gb_fmi_index_info(gb_fmi_index *idx, int64_t *n, int64_t *count5, int64_t *sentinel) {
+  GB_ARG(idx, "gb_fmi_index_info: null index");
+  if (n) *n = idx->n;
+  if (count5)
+    for (int b = 0; b < 5; b++) count5[b] = idx->count[b];
+  if (sentinel) *sentinel = idx->sentinel;
+  return GB_OK;
+}
+
+int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes) {
+  GB_ARG(idx && dst, "gb_fmi_index_cp_occ: null argument");
+  const int64_t bytes = idx->cp_size * (int64_t)sizeof(gbfmi::CpOcc);
+  GB_ARG(dst_bytes >= bytes, "gb_fmi_index_cp_occ: need %lld bytes", (long long)bytes);
+  GB_HIP(hipMemcpy(dst, idx->d_occ, (size_t)bytes, hipMemcpyDeviceToHost));
+  return GB_OK;
+}
+
+int gb_fmi_index_destroy(gb_fmi_index *idx) {
+  if (!idx) return GB_OK;
+  (void)hipFree(idx->d_occ);
+  delete idx;
+  return GB_OK;
+}
+
+int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens,
+                        int32_t num_reads, int32_t max_readlength, gb_fmi_reads **out) {
+  GB_ARG(idx && out && (num_reads == 0 || (enc_qdb && lens)), "gb_fmi_reads_create: null argument");
+  GB_ARG(num_reads >= 0 && max_readlength > 0 && max_readlength < 10000,
+         "gb_fmi_reads_create: bad sizes (reads %d, max_readlength %d)", num_reads, max_readlength);
+  for (int32_t r = 0; r < num_reads; r++)
+    GB_ARG(lens[r] >= 0 && lens[r] <= max_readlength, "read %d: length %d > max_readlength %d", r,
+           lens[r], max_readlength);
+  *out = nullptr;
+  auto *R = new gb_fmi_reads();
+  R->idx = idx;
+  R->nreads = num_reads;
+  R->stride = max_readlength;
+  R->lanes = lanes_for_device();
+  const size_t nr = (size_t)std::max(num_reads, 1);
+  hipError_t e = hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking);
+  for (auto &ev : R->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e == hipSuccess) e = hipMalloc(&R->d_qdb, nr * (size_t)max_readlength);
+  if (e == hipSuccess) e = hipMalloc(&R->d_lens, nr * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::Ent));
+  if (e == hipSuccess) e = hipMalloc(&R->d_slots, nr * gbfmi::kCap * sizeof(gb_smem));
+  if (e == hipSuccess) e = hipMalloc(&R->d_counts, nr * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_phase, nr * 3 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_offsets, (nr + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 4 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_calls, sizeof(unsigned long long));
+  if (e == hipSuccess)
+    e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
+  if (e == hipSuccess) e = hipMalloc(&R->d_temp, std::max<size_t>(R->temp_bytes, 16));
+  if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
+  if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_lens, lens, (size_t)num_reads * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    gb::set_error("gb_fmi_reads_create: %s", hipGetErrorString(e));
+    gb_fmi_reads_destroy(R);
+    return GB_ERR_HIP;
+  }
+  *out = R;
+  return GB_OK;
+}
+
+int gb_fmi_reads_destroy(gb_fmi_reads *R) {
+  if (!R) return GB_OK;
+  if (R->stream) (void)hipStreamSynchronize(R->stream);
+  for (void *p : {(void *)R->d_qdb, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
+                  (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
+                  (void *)R->d_ctl, (void *)R->d_calls, R->d_temp})
+    (void)hipFree(p);
+  for (auto ev : R->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (R->stream) (void)hipStreamDestroy(R->stream);
+  delete R;
+  return GB_OK;
+}
+
+int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
+  GB_ARG(R, "gb_fmi_search: null read set");
+  GB_ARG(min_seed_len > 0, "gb_fmi_search: min_seed_len %d", min_seed_len);
+  GB_HIP(hipSetDevice(R->idx->device));
+  GB_HIP(hipEventRecord(R->ev[0], R->stream));
+  GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
+  GB_HIP(hipMemsetAsync(R->d_calls, 0, sizeof(unsigned long long), R->stream));
+  gbfmi::SearchArgs A;
+  A.F.occ = R->idx->d_occ;
+  for (int b = 0; b < 5; b++) A.F.count[b] = R->idx->count[b];
+  A.F.sentinel = R->idx->sentinel;
+  A.qdb = R->d_qdb;
+  A.lens = R->d_lens;
+  A.nreads = R->nreads;
+  A.stride = R->stride;
+  A.min_seed_len = min_seed_len;
+  A.split_len = (int)(min_seed_len * 1.5 + .499);  // fmi.cpp:239
+  A.scratch = R->d_scratch;
+  A.slots = R->d_slots;
+  A.counts = R->d_counts;
+  A.phase = R->d_phase;
+  A.next_read = R->d_ctl;
+  A.overflow = R->d_ctl + 1;
+  A.bwt_calls = R->d_calls;
+  if (R->nreads > 0) {
+    const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
+    hipLaunchKernelGGL(gbfmi::smem_search, dim3(blocks), dim3(64), 0, R->stream, A);
+    GB_HIP(hipGetLastError());
+  }
+  GB_HIP(hipEventRecord(R->ev[1], R->stream));
+  if (R->nreads > 0) {
+    GB_HIP(hipcub::DeviceScan::ExclusiveSum(R->d_temp, R->temp_bytes, R->d_counts, R->d_offsets,
+                                            R->nreads, R->stream));
+  }
+  GB_HIP(hipEventRecord(R->ev[2], R->stream));
+  R->ran = true;
+  return GB_OK;
+}
+
+int gb_fmi_sync(gb_fmi_reads *R) {
+  GB_ARG(R, "gb_fmi_sync: null read set");
+  GB_HIP(hipStreamSynchronize(R->stream));
+  return GB_OK;
+}
+
+int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t out_cap,
+                   int64_t *total, int64_t *batch_counts, int64_t *phase_counts) {
+  GB_ARG(R && R->ran, "gb_fmi_results: search has not run");
+  GB_ARG(batch_size > 0, "gb_fmi_results: batch_size %d", batch_size);
+  GB_HIP(hipSetDevice(R->idx->device));
+  GB_HIP(hipStreamSynchronize(R->stream));
+  int32_t ctl[4];
+  GB_HIP(hipMemcpy(ctl, R->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+  if (ctl[1] != 0) {
+    gb::set_error("gb_fmi_results: %d reads exceeded %d SMEM slots", ctl[1], gbfmi::kCap);
+    return GB_ERR_STATE;
+  }
+  const int32_t n = R->nreads;
+  std::vector<int32_t> counts((size_t)std::max(n, 1)), phase((size_t)std::max(n, 1) * 3);
+  if (n) {
+    GB_HIP(hipMemcpy(counts.data(), R->d_counts, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    GB_HIP(hipMemcpy(phase.data(), R->d_phase, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost));
+  }
+  int64_t tot = 0;
+  for (int32_t r = 0; r < n; r++) tot += counts[r];
+  if (total) *total = tot;
+  if (batch_counts) {
+    for (int32_t b = 0; b * (int64_t)batch_size < n; b++) {
+      int64_t s = 0;
+      for (int32_t r = b * batch_size; r < std::min<int64_t>(n, (int64_t)(b + 1) * batch_size); r++) s += counts[r];
+      batch_counts[b] = s;
+    }
+  }
+  if (phase_counts) {
+    phase_counts[0] = phase_counts[1] = phase_counts[2] = 0;
+    for (int32_t r = 0; r < n; r++)
+      for (int k = 0; k < 3; k++) phase_counts[k] += phase[3 * r + k];
+  }
+  if (out) {
+    GB_ARG(out_cap >= tot, "gb_fmi_results: out_cap %lld < %lld SMEMs", (long long)out_cap, (long long)tot);
+    if (tot > R->out_cap) {
+      (void)hipFree(R->d_out);
+      R->d_out = nullptr;
+      GB_HIP(hipMalloc(&R->d_out, sizeof(gb_smem) * (size_t)tot));
+      R->out_cap = tot;
+    }
+    if (tot) {
+      hipLaunchKernelGGL(gbfmi::scatter_smems, dim3((n + 255) / 256), dim3(256), 0, R->stream,
+                         R->d_slots, R->d_counts, R->d_offsets, R->d_out, n);
+      GB_HIP(hipGetLastError());
+      GB_HIP(hipMemcpyAsync(out, R->d_out, sizeof(gb_smem) * (size_t)tot, hipMemcpyDeviceToHost, R->stream));
+      GB_HIP(hipStreamSynchronize(R->stream));
+    }
+  }
+  return GB_OK;
+}
+
+int gb_fmi_timing(gb_fmi_reads *R, float *search_ms, float *total_ms, int64_t *bwt_calls) {
+  GB_ARG(R && R->ran, "gb_fmi_timing: search has not run");
+  GB_HIP(hipEventSynchronize(R->ev[2]));
+  float a = 0, b = 0;
+  GB_HIP(hipEventElapsedTime(&a, R->ev[0], R->ev[1]));
+  GB_HIP(hipEventElapsedTime(&b, R->ev[0], R->ev[2]));
+  if (search_ms) *search_ms = a;
+  if (total_ms) *total_ms = b;
+  if (bwt_calls) {
+    unsigned long long c = 0;
+    GB_HIP(hipMemcpy(&c, R->d_calls, sizeof(c), hipMemcpyDeviceToHost));
+    *bwt_calls = (int64_t)c;
+  }
+  return GB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,26 @@
+// fmi_index.h -- device-side FM-index representation shared by the index builder and the search.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gbfmi {
+
+// CP_OCC (tools/bwa-mem2/src/FMI_search.h:59-63): occurrence counts before row 64*i and one-hot
+// bit planes (MSB = first row of the block) for BWT rows [64i, 64i+64).
+struct __attribute__((aligned(64))) CpOcc {
+  int64_t cp_count[4];
+  uint64_t one_hot_bwt_str[4];
+};
+static_assert(sizeof(CpOcc) == 64, "CP_OCC is 64 bytes");
+
+}  // namespace gbfmi
+
+// Index object behind the C ABI (one per device).
+struct gb_fmi_index {
+  int device = -1;
+  int64_t n = 0;            // reference_seq_len = |text| + 1
+  int64_t count[5] = {0};   // after the load-time +1 (FMI_search.cpp:763-768)
+  int64_t sentinel = -1;
+  int64_t cp_size = 0;      // (n >> 6) + 1 entries
+  gbfmi::CpOcc *d_occ = nullptr;
+};

@@ -1,7 +1,7 @@
 // gb_common.cpp -- error state and device selection shared by every gb_* entry point.
 #include "gb_common.h"
 
-#include "../../include/gb_phmm.h"
+#include "../../include/gb.h"
 
 namespace gb {
 static thread_local std::string g_err;

@@ -103,3 +103,89 @@ def write_phmm_file(path, batches):
                 f.write(f"{bases.decode()} {enc(q)} {enc(i)} {enc(d)} {enc(c)}\n")
             for h in b.haps:
                 f.write(h.decode() + "\n")
+
+
+# ---------------------------------------------------------------------------------------------
+# fmi: synthetic reference + reads ('large' = 10 M x 151 bp reads over a 512 Mbp
+# reference (+RC); 1% substitutions, 0.1% indels, 0.05% N; seed 7)
+# ---------------------------------------------------------------------------------------------
+def fmi_reference(length: int, seed: int = 7, repeat_frac: float = 0.08):
+    """Random A/C/G/T codes (0..3) with genome-like structure: ~repeat_frac of the sequence is
+    overwritten by mutated copies of earlier segments (interspersed repeats) and short tandem
+    repeats, so the SMEM search sees multi-copy intervals and reseeding, not only unique hits."""
+    rng = np.random.default_rng(seed)
+    ref = rng.integers(0, 4, length, dtype=np.uint8)
+    budget = int(length * repeat_frac)
+    while budget > 0 and length > 1000:
+        if rng.random() < 0.85:  # interspersed copy, 1-15% divergence
+            L = int(min(length // 4, max(50, rng.geometric(1 / 800))))
+            src = int(rng.integers(0, length - L))
+            dst = int(rng.integers(0, length - L))
+            seg = ref[src:src + L].copy()
+            mut = rng.random(L) < rng.uniform(0.0, 0.15)
+            seg[mut] = rng.integers(0, 4, int(mut.sum()), dtype=np.uint8)
+            if rng.random() < 0.5:
+                seg = (3 - seg[::-1]).astype(np.uint8)
+        else:  # tandem repeat of a short unit
+            unit = rng.integers(0, 4, int(rng.integers(1, 7)), dtype=np.uint8)
+            L = int(rng.integers(20, 300))
+            seg = np.resize(unit, L)
+            dst = int(rng.integers(0, length - L))
+        ref[dst:dst + len(seg)] = seg
+        budget -= len(seg)
+    return ref
+
+
+def fmi_reads(ref: np.ndarray, num_reads: int, read_len: int = 151, seed: int = 7, sub_rate=0.01,
+              indel_rate=0.001, n_rate=0.0005):
+    """Reads sampled uniformly from both strands; returns (codes[num_reads, read_len] uint8 with
+    4 = N, lens int32). Codes follow fmi.cpp:141-177 (A0 C1 G2 T3, anything else 4)."""
+    rng = np.random.default_rng(seed)
+    G = len(ref)
+    out = np.empty((num_reads, read_len), np.uint8)
+    starts = rng.integers(0, G - read_len - 8, num_reads)
+    strand = rng.random(num_reads) < 0.5
+    span = read_len + 8
+    idx = starts[:, None] + np.arange(span)[None, :]
+    frag = ref[idx]
+    # indels: per read at most a couple, applied on the fragment before trimming
+    for r in np.nonzero(rng.random(num_reads) < indel_rate * read_len)[0]:
+        p = int(rng.integers(1, read_len - 1))
+        if rng.random() < 0.5:
+            frag[r, p:-1] = frag[r, p + 1:].copy()
+        else:
+            frag[r, p + 1:] = frag[r, p:-1].copy()
+            frag[r, p] = rng.integers(0, 4)
+    frag = frag[:, :read_len]
+    frag[strand] = (3 - frag[strand, ::-1])
+    sub = rng.random(frag.shape) < sub_rate
+    frag[sub] = (frag[sub] + rng.integers(1, 4, int(sub.sum()))) % 4
+    nm = rng.random(frag.shape) < n_rate
+    frag[nm] = 4
+    out[:] = frag
+    return out, np.full(num_reads, read_len, np.int32)
+
+
+def write_fasta(path, ref: np.ndarray, name="chr1", width=80):
+    s = np.frombuffer(b"ACGT", np.uint8)[ref].tobytes()
+    with open(path, "wb") as f:
+        f.write(b">" + name.encode() + b"\n")
+        for i in range(0, len(s), width):
+            f.write(s[i:i + width] + b"\n")
+
+
+def write_fastq(path, codes: np.ndarray, lens: np.ndarray):
+    lut = np.frombuffer(b"ACGTN", np.uint8)
+    with open(path, "wb") as f:
+        for r in range(len(lens)):
+            s = lut[codes[r, :lens[r]]].tobytes()
+            f.write(b"@r%d\n%s\n+\n%s\n" % (r, s, b"I" * len(s)))
+
+
+def read_pac(path):
+    """pac2nt (FMI_search.cpp:93-169): forward-strand codes from a bwa .pac file."""
+    raw = np.fromfile(path, np.uint8)
+    seq_len = (len(raw) - 2) * 4 + int(raw[-1])  # pac_seq_len: (ftell(-1) - 1) * 4 + last byte
+    b = raw[: (seq_len + 3) // 4]
+    codes = np.stack([(b >> 6) & 3, (b >> 4) & 3, (b >> 2) & 3, b & 3], axis=1).reshape(-1)
+    return codes[:seq_len].astype(np.uint8)

@@ -1,0 +1,74 @@
+/*
+ * gb_fmi.h -- C ABI of the MI355X bwa-mem2 FM-index SMEM search (drop-in boundary for benchmarks/fmi).
+ *
+ * Reference interface this replaces (paths relative to the reference repo):
+ *   class FMI_search (tools/bwa-mem2/src/FMI_search.h:101-224):
+ *     FMI_search(const char *fname); load_index();                 FMI_search.cpp:469-984
+ *     getSMEMsAllPosOneThread(...)                                  FMI_search.cpp:1182-1241
+ *     getSMEMsOnePosOneThread(...)                                  FMI_search.cpp:986-1180
+ *     bwtSeedStrategyAllPosOneThread(...)                           FMI_search.cpp:1243-1326
+ *     sortSMEMs(...)                                                FMI_search.cpp:1520-1534
+ *     build_index()                                                 FMI_search.cpp:358-434
+ *   driven per batch by benchmarks/fmi/fmi.cpp:253-348 (smem1 -> reseed -> LAST -> rid offset -> sort).
+ * gb_fmi_search() runs that whole per-batch pipeline for every read on the GPU; the per-method entry
+ * points serve the FMI_search adapter (include/fmi_search_gpu.h) one call at a time.
+ *
+ * Plain pointers and sizes; 0 on success, negative gb_status on failure (gb_last_error()).
+ */
+#ifndef GB_FMI_H
+#define GB_FMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gb.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same 40-byte layout as the reference SMEM (FMI_search.h:91-99, non-DEBUG build). */
+typedef struct gb_smem {
+  uint32_t rid, m, n;
+  int64_t k, l, s;
+} gb_smem;
+
+typedef struct gb_fmi_index gb_fmi_index;
+
+/* load_index(): reads <prefix>.bwt.2bit.64 (reference file format) into HBM. */
+int gb_fmi_index_load(const char *bwt_2bit_64_path, gb_fmi_index **out);
+/* build_index() on the GPU from forward-strand codes (0..3 = A,C,G,T; pac2nt order): text =
+ * ref + reverse complement, suffix array, BWT, CP_OCC checkpoints, sampled SA. out_path (nullable)
+ * receives the reference-format .bwt.2bit.64 file. */
+int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, const char *out_path,
+                       gb_fmi_index **out);
+/* n = reference_seq_len (|text|+1), count[5] as used by the search (load-time +1 applied). */
+int gb_fmi_index_info(gb_fmi_index *idx, int64_t *n, int64_t *count5, int64_t *sentinel_index);
+/* Copies the CP_OCC table (64 bytes per 64 BWT rows, reference layout) to host memory. */
+int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes);
+int gb_fmi_index_destroy(gb_fmi_index *idx);
+
+/* Device-resident read set: enc_qdb is numReads x max_readlength codes (A0 C1 G2 T3, else 4;
+ * fmi.cpp:141-177), lens[r] = read length. */
+typedef struct gb_fmi_reads gb_fmi_reads;
+int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens,
+                        int32_t num_reads, int32_t max_readlength, gb_fmi_reads **out);
+int gb_fmi_reads_destroy(gb_fmi_reads *r);
+
+/* The fmi.cpp per-batch pipeline over every read (asynchronous on the read set's stream):
+ * SMEMs (min_intv 1), reseeding (split_len = (int)(min_seed_len*1.5+.499), split width 10),
+ * LAST seeds (max_intv 20, min length min_seed_len+1), per-read sort by (m asc, n desc). */
+int gb_fmi_search(gb_fmi_reads *r, int32_t min_seed_len);
+/* Results of the last search: SMEMs in (rid, m, n desc) order with rid = read index, i.e. the
+ * concatenation of the reference's sorted batches. batch_counts[b] = numTotalSmem of batch b
+ * (batch_size reads per batch); phase_counts = {num_smem1, num_smem2, num_smem3} summed. */
+int gb_fmi_results(gb_fmi_reads *r, int32_t batch_size, gb_smem *out, int64_t out_cap,
+                   int64_t *total, int64_t *batch_counts, int64_t *phase_counts);
+/* Kernel time of the last search (HIP events on the read set's stream), ms; backwardExt calls. */
+int gb_fmi_timing(gb_fmi_reads *r, float *search_ms, float *total_ms, int64_t *bwt_calls);
+int gb_fmi_sync(gb_fmi_reads *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GB_FMI_H */

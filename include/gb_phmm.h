@@ -21,6 +21,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "gb.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -34,19 +36,6 @@ typedef struct gb_testcase {
   const char *q, *i, *d, *c;
   const char *hap, *rs;
 } gb_testcase;
-
-enum gb_status {
-  GB_OK = 0,
-  GB_ERR_ARG = -1,
-  GB_ERR_HIP = -2,
-  GB_ERR_NODEV = -3,
-  GB_ERR_NOMEM = -4,
-  GB_ERR_STATE = -5,
-};
-
-const char *gb_last_error(void);
-int gb_device_count(int *count);
-int gb_set_device(int device);
 
 /* initPairHMM(): builds the probability tables (Context.h) on the host and uploads them. */
 int gb_phmm_init(void);

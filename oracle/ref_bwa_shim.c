@@ -1,0 +1,83 @@
+/* oracle/ref_bwa_shim.c -- TEST INFRASTRUCTURE ONLY.
+ * Our own thin C entry points over the reference tree's UNMODIFIED bwa v1 sources
+ * (/root/reference/tools/bwa, compiled by oracle/Makefile into oracle/_ref/libref_bwa.so), used as
+ * an independent cross-check of the bwa-mem2 SMEM restatement (oracle/fmi_oracle.c): bwa-mem2's
+ * SMEM search reproduces bwa-mem's, on the same forward+reverse-complement text.
+ *   index     bwa_idx_build (tools/bwa/bwtindex.c:256) -> .pac/.bwt; bwt_restore_bwt (bwt.c:443)
+ *   SMEMs     mem_collect_intv (tools/bwa/bwamem.c:114-162) restated below over bwt_smem1
+ *             (bwt.c:353) and bwt_seed_strategy1 (bwt.c:358), without the final sort.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "bwt.h"
+#include "kvec.h"
+
+int bwa_idx_build(const char *fa, const char *prefix, int algo_type, int block_size);
+extern int bwa_verbose;
+
+int ref_bwa_build(const char *fasta, const char *prefix) {
+  bwa_verbose = 1;
+  return bwa_idx_build(fasta, prefix, 0, 10000000);
+}
+
+void *ref_bwa_load(const char *bwt_path) { return bwt_restore_bwt(bwt_path); }
+void ref_bwa_free(void *bwt) { bwt_destroy((bwt_t *)bwt); }
+
+/* mem_collect_intv with opt = {min_seed_len, split_factor 1.5, split_width 10, max_mem_intv 20}.
+ * Out: k, l, s, m (start), n (end, inclusive) for every interval; returns count or -1 on overflow. */
+int64_t ref_bwa_collect(void *bwtp, const uint8_t *seq, int len, int min_seed_len, int64_t *k,
+                        int64_t *l, int64_t *s, int32_t *m, int32_t *n, int64_t cap) {
+  const bwt_t *bwt = (const bwt_t *)bwtp;
+  bwtintv_v mem = {0, 0, 0}, mem1 = {0, 0, 0}, t0 = {0, 0, 0}, t1 = {0, 0, 0};
+  bwtintv_v *tmpv[2] = {&t0, &t1};
+  int i, x = 0, old_n, kk;
+  int split_len = (int)(min_seed_len * 1.5 + .499);
+  while (x < len) {
+    if (seq[x] < 4) {
+      x = bwt_smem1(bwt, len, seq, x, 1, &mem1, tmpv);
+      for (i = 0; i < (int)mem1.n; ++i) {
+        bwtintv_t *p = &mem1.a[i];
+        int slen = (uint32_t)p->info - (p->info >> 32);
+        if (slen >= min_seed_len) kv_push(bwtintv_t, mem, *p);
+      }
+    } else
+      ++x;
+  }
+  old_n = (int)mem.n;
+  for (kk = 0; kk < old_n; ++kk) {
+    bwtintv_t *p = &mem.a[kk];
+    int start = p->info >> 32, end = (int32_t)p->info;
+    if (end - start < split_len || p->x[2] > 10) continue;
+    bwt_smem1(bwt, len, seq, (start + end) >> 1, p->x[2] + 1, &mem1, tmpv);
+    for (i = 0; i < (int)mem1.n; ++i)
+      if ((uint32_t)mem1.a[i].info - (mem1.a[i].info >> 32) >= (uint32_t)min_seed_len)
+        kv_push(bwtintv_t, mem, mem1.a[i]);
+  }
+  x = 0;
+  while (x < len) {
+    if (seq[x] < 4) {
+      bwtintv_t mm;
+      x = bwt_seed_strategy1(bwt, len, seq, x, min_seed_len, 20, &mm);
+      if (mm.x[2] > 0) kv_push(bwtintv_t, mem, mm);
+    } else
+      ++x;
+  }
+  int64_t cnt = (int64_t)mem.n;
+  if (cnt <= cap) {
+    for (int64_t q = 0; q < cnt; q++) {
+      k[q] = (int64_t)mem.a[q].x[0];
+      l[q] = (int64_t)mem.a[q].x[1];
+      s[q] = (int64_t)mem.a[q].x[2];
+      m[q] = (int32_t)(mem.a[q].info >> 32);
+      n[q] = (int32_t)((uint32_t)mem.a[q].info) - 1;
+    }
+  } else {
+    cnt = -1;
+  }
+  free(mem.a);
+  free(mem1.a);
+  free(t0.a);
+  free(t1.a);
+  return cnt;
+}

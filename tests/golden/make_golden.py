@@ -75,7 +75,40 @@ def phmm_inputs(seed=2024):
     return reads, haps, pairs
 
 
+def fmi_golden():
+    """fmi_golden.npz: a 200 kbp genome-like reference, 600 reads (with N's, indels, a short read, an
+    all-N read) and the SMEM intervals bwa v1's own code computes for them (tools/bwa/bwt.c
+    bwt_smem1/bwt_seed_strategy1 driven like mem_collect_intv, bwamem.c:114-162), which bwa-mem2's
+    SMEM search reproduces (cross-checked against oracle/fmi_oracle.c)."""
+    import tempfile
+    import fmi_util
+    lib = fmi_util.ref_bwa()
+    if lib is None:
+        raise SystemExit("oracle/_ref/libref_bwa.so missing: run `make -C oracle ref` first")
+    ref = gen.fmi_reference(200_000, seed=11)
+    codes, lens = gen.fmi_reads(ref, 600, read_len=151, seed=12, sub_rate=0.02, n_rate=0.002)
+    lens = lens.copy()
+    lens[5] = 17            # shorter than min_seed_len
+    lens[6] = 60
+    codes[7, :] = 4         # all N
+    codes[8, :] = 0         # poly-A
+    with tempfile.TemporaryDirectory() as d:
+        gen.write_fasta(d + "/ref.fa", ref)
+        assert lib.ref_bwa_build((d + "/ref.fa").encode(), (d + "/ref").encode()) == 0
+        pac = gen.read_pac(d + "/ref.pac")
+        assert (pac == ref).all()
+        bwt = lib.ref_bwa_load((d + "/ref.bwt").encode())
+        per = fmi_util.bwa_smems(lib, bwt, codes, lens)
+        lib.ref_bwa_free(bwt)
+    rid = np.concatenate([[r] * len(x) for r, x in enumerate(per)]).astype(np.int32)
+    flat = np.array([e for x in per for e in x], np.int64).reshape(-1, 5)
+    np.savez_compressed(os.path.join(HERE, "fmi_golden.npz"), ref=ref, codes=codes, lens=lens,
+                        rid=rid, m=flat[:, 0], n=flat[:, 1], k=flat[:, 2], l=flat[:, 3], s=flat[:, 4])
+    print("wrote fmi_golden.npz:", len(rid), "SMEMs for", len(lens), "reads")
+
+
 def main():
+    fmi_golden()
     ref = oracle_lib.ref_phmm()
     if ref is None:
         raise SystemExit("oracle/_ref/libref_phmm.so missing: run `make -C oracle ref` first")
