@@ -4,10 +4,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batches B] [--no-cpu-baseline]
 
 Metric (BASELINE.json): "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X".
-A step = one PairHMM forward pass (f32 kernel + f64 fallback kernel + log10 epilogue) over one
-'large'-shaped synthetic job of B batches (gen.phmm_dataset, seed 1 + rank) already resident in HBM.
-`value` = total cells of all ranks x K / max-over-ranks wall time of the K timed steps, in GCUPS.
-Weak scaling: every rank processes its own job of the same shape (independent shards, no
+phmm (the line's `value`): a step = one PairHMM forward pass (f32 kernel + f64 fallback kernel +
+log10 epilogue) over one 'large'-shaped synthetic job of B batches (gen.phmm_dataset, seed 1 + rank)
+already resident in HBM; value = total cells of all ranks x K / max-over-ranks wall time, in GCUPS.
+fmi (the line's "fmi" object): a step = the whole fmi.cpp per-batch pipeline (SMEMs, reseeding,
+LAST seeds, per-read sort) over every read of the rank's shard (gen.fmi_reads, seed 8 + rank) against
+a 512 Mbp genome-like synthetic reference (+RC: 1.024 G BWT rows, 1.02 GB CP_OCC) built on the GPU;
+value = reads of all ranks x K / max-over-ranks wall time, in Mreads/s.
+Weak scaling: every rank processes its own shard of the same shape (independent shards, no
 data-path collective; torch.distributed only provides the barrier and the max-time reduction).
 """
 from __future__ import annotations
@@ -28,6 +32,8 @@ sys.path.insert(0, ROOT)
 PEAK_F32_OPS = 256 * 4 * 32 * 2.4e9  # non-FMA FP32 VALU ops/s = 78.6e12 (157.3 TF counts FMA as 2)
 PEAK_F64_OPS = PEAK_F32_OPS / 2      # FP64 vector peak 78.6 TF (FMA=2) -> 39.3e12 non-FMA ops/s
 PHMM_FLOP_PER_CELL = 12              # 12 FP ops per cell, no FMA
+PEAK_HBM = 8.0e12                    # HBM3E spec bytes/s (MI355X_MICROARCH.md)
+FMI_BYTES_PER_EXT = 128              # 2 x 64-B CP_OCC lines per backwardExt
 
 
 def dist_env():
@@ -129,29 +135,37 @@ def cpu_baseline_phmm(ta, sample_seconds: float):
                       f"job x {reps} passes, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batches", type=int, default=16, help="'large' batches per job (per rank)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+def cpu_baseline_fmi(oracle_index, codes, lens, sample_seconds: float):
+    """The bwa-mem2 SMEM restatement (oracle/fmi_oracle.c, kind 'port': the reference FMI_search.cpp
+    is not buildable here without Palisade) over a bounded sample of the same reads."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    cal = min(len(lens), 4000 * threads)
+    t0 = time.perf_counter()
+    oracle_index.run_threaded(codes[:cal], lens[:cal], threads)
+    rate = cal / max(time.perf_counter() - t0, 1e-6)
+    m = int(min(len(lens), max(cal, rate * sample_seconds)))
+    t0 = time.perf_counter()
+    oracle_index.run_threaded(codes[:m], lens[:m], threads)
+    t = time.perf_counter() - t0
+    return {"value": m / t / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
+            "sample": f"first {m} of {len(lens)} reads of the same shard, C restatement of bwa-mem2 "
+                      f"FMI_search (batches of 512 over {threads} threads), {t:.1f} s"}
 
-    world, rank, local = dist_env()
-    D = Dist(world)
-    import genomicsbench_palisade_amd as gb
+
+def bench_phmm(args, D, rank, world):
+    import genomicsbench_palisade_amd as gb  # noqa: F401
     from genomicsbench_palisade_amd import gen, phmm
     from genomicsbench_palisade_amd._tc import TestcaseArray
 
-    gb.set_device(local)
     phmm.init_pairhmm()
     batches = gen.phmm_dataset("large", args.batches, seed=1 + rank)
     ta = TestcaseArray.from_batches(batches)
     job = phmm.DeviceBatch(ta)
     ntc, cells, _ = job.stats()
-
     for _ in range(args.warmup):
         job.run()
         job.sync()
@@ -175,42 +189,125 @@ def main():
     elapsed = D.max(time.perf_counter() - t0)
     total_cells = D.sum(float(cells)) * args.steps
     gcups = total_cells / elapsed / 1e9
-
     ms32, ms64 = float(np.mean(k32)), float(np.mean(k64))
     if ms32 >= ms64:
         kern, ach, peak = "phmm_forward<float>", PHMM_FLOP_PER_CELL * cells / (ms32 * 1e-3), PEAK_F32_OPS
     else:
         kern, ach, peak = "phmm_forward<double>", PHMM_FLOP_PER_CELL * cells_f64 / (ms64 * 1e-3), PEAK_F64_OPS
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
+    job.close()
+    return {
+        "value": gcups, "elapsed": elapsed, "ntc": ntc, "cells": cells, "f64_frac": float(used.mean()),
+        "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
+                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": None},
+        "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
+        "cpu_baseline": cpu,
+    }
+
+
+def bench_fmi(args, D, rank, world):
+    from genomicsbench_palisade_amd import fmi, gen
+
+    t0 = time.perf_counter()
+    ref = gen.fmi_reference(int(args.fmi_ref_mbp * 1e6), seed=7)  # same reference on every rank
+    idx = fmi.Index.build(ref)
+    t_index = time.perf_counter() - t0
+    codes, lens = gen.fmi_reads(ref, args.fmi_reads, read_len=151, seed=8 + rank)
+    rs = fmi.Reads(idx, codes, lens)
+    for _ in range(args.warmup):
+        rs.search(19)
+        rs.sync()
+    _, total, _, phases = rs.results(batch_size=512, want_smems=False)
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    ks, kt, calls = [], [], 0
+    for _ in range(args.steps):
+        rs.search(19)
+        rs.sync()
+        a, b, calls = rs.timing()
+        ks.append(a)
+        kt.append(b)
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    mreads = D.sum(float(len(lens))) * args.steps / elapsed / 1e6
+    ms = float(np.mean(ks))
+    alg_bytes = calls * FMI_BYTES_PER_EXT + len(lens) * 151 + total * 40
+    ach = alg_bytes / (ms * 1e-3)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import fmi_util
+        oi = fmi_util.OracleIndex(ref)
+        cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds)
+        oi.close()
+    n, _, _ = idx.info()
+    rs.close()
+    idx.close()
+    return {
+        "value": round(mreads, 3), "unit": "Mreads/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": f"fmi large: {args.fmi_ref_mbp:g} Mbp synthetic genome-like reference "
+                               f"(BWT rows {n}), {len(lens)} reads x 151 bp/rank, minSeedLen 19, batch 512",
+                   "smems_per_read": total / len(lens), "num_smem1_2_3": [int(x) for x in phases],
+                   "backwardExt_per_read": calls / len(lens), "index_build_s": round(t_index, 2)},
+        "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
+                     "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": None,
+                     "algorithmic_bytes": int(alg_bytes)},
+        "kernels_ms": {"smem_search": ms, "smem_search+scan": float(np.mean(kt))},
+        "cpu_baseline": cpu,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batches", type=int, default=16, help="'large' phmm batches per job (per rank)")
+    ap.add_argument("--fmi-reads", type=int, default=10_000_000, help="fmi reads per rank")
+    ap.add_argument("--fmi-ref-mbp", type=float, default=512.0)
+    ap.add_argument("--only", choices=["phmm", "fmi"], default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    D = Dist(world)
+    import genomicsbench_palisade_amd as gb
+    gb.set_device(local)
+
+    ph = bench_phmm(args, D, rank, world) if args.only != "fmi" else None
+    fm = bench_fmi(args, D, rank, world) if args.only != "phmm" else None
 
     if rank == 0:
         line = {
             "metric": "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X",
-            "value": round(gcups, 3),
+            "value": round(ph["value"], 3) if ph else None,
             "unit": "GCUPS (phmm)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ph["elapsed"] / args.steps * 1e3, 4) if ph else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32+f64",
-            "data": "synthetic ('large'-shaped PairHMM batches, gen.phmm_dataset seed 1+rank)",
-            "config": {"workload": "phmm large: %d batches/rank, %d testcases, %.3f G cells/rank/step,"
-                                   " %.1f%% testcases on the f64 fallback" % (
-                                       args.batches, ntc, cells / 1e9, 100.0 * used.mean()),
+            "dtype": "f32+f64 (phmm), int64 (fmi)",
+            "data": "synthetic ('large'-shaped PairHMM batches seed 1+rank; genome-like reference seed 7 "
+                    "+ 151 bp reads seed 8+rank for fmi)",
+            "config": {"workload": ("phmm large: %d batches/rank, %d testcases, %.3f G cells/rank/step, "
+                                    "%.1f%% testcases on the f64 fallback" % (
+                                        args.batches, ph["ntc"], ph["cells"] / 1e9, 100 * ph["f64_frac"]))
+                       if ph else None,
                        "parallelism": f"shard{world}"},
-            "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
-                         "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": None},
-            "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
-            "cpu_baseline": cpu,
+            "roofline": ph["roofline"] if ph else None,
+            "kernels_ms": ph["kernels_ms"] if ph else None,
+            "cpu_baseline": ph["cpu_baseline"] if ph else None,
+            "fmi": fm,
         }
         print(json.dumps(line))
-    job.close()
     D.close()
 
 

@@ -137,32 +137,37 @@ def fmi_reference(length: int, seed: int = 7, repeat_frac: float = 0.08):
 
 
 def fmi_reads(ref: np.ndarray, num_reads: int, read_len: int = 151, seed: int = 7, sub_rate=0.01,
-              indel_rate=0.001, n_rate=0.0005):
+              indel_rate=0.001, n_rate=0.0005, chunk: int = 250_000):
     """Reads sampled uniformly from both strands; returns (codes[num_reads, read_len] uint8 with
-    4 = N, lens int32). Codes follow fmi.cpp:141-177 (A0 C1 G2 T3, anything else 4)."""
+    4 = N, lens int32). Codes follow fmi.cpp:141-177 (A0 C1 G2 T3, anything else 4). Generated in
+    chunks so 10 M-read sets stay within a few GB of host memory."""
     rng = np.random.default_rng(seed)
     G = len(ref)
     out = np.empty((num_reads, read_len), np.uint8)
-    starts = rng.integers(0, G - read_len - 8, num_reads)
-    strand = rng.random(num_reads) < 0.5
     span = read_len + 8
-    idx = starts[:, None] + np.arange(span)[None, :]
-    frag = ref[idx]
-    # indels: per read at most a couple, applied on the fragment before trimming
-    for r in np.nonzero(rng.random(num_reads) < indel_rate * read_len)[0]:
-        p = int(rng.integers(1, read_len - 1))
-        if rng.random() < 0.5:
-            frag[r, p:-1] = frag[r, p + 1:].copy()
-        else:
-            frag[r, p + 1:] = frag[r, p:-1].copy()
-            frag[r, p] = rng.integers(0, 4)
-    frag = frag[:, :read_len]
-    frag[strand] = (3 - frag[strand, ::-1])
-    sub = rng.random(frag.shape) < sub_rate
-    frag[sub] = (frag[sub] + rng.integers(1, 4, int(sub.sum()))) % 4
-    nm = rng.random(frag.shape) < n_rate
-    frag[nm] = 4
-    out[:] = frag
+    for c0 in range(0, num_reads, chunk):
+        nr = min(chunk, num_reads - c0)
+        starts = rng.integers(0, G - span, nr)
+        strand = rng.random(nr) < 0.5
+        frag = ref[starts[:, None] + np.arange(span)[None, :]]
+        # indels: at most one per read, applied on the fragment before trimming (vectorized)
+        R = np.nonzero(rng.random(nr) < indel_rate * read_len)[0]
+        if len(R):
+            p = rng.integers(1, read_len - 1, len(R))[:, None]
+            dele = (rng.random(len(R)) < 0.5)[:, None]
+            col = np.arange(span)[None, :]
+            src = np.where(dele, np.minimum(col + (col >= p), span - 1), col - (col > p))
+            sub_frag = np.take_along_axis(frag[R], src, axis=1)
+            ins_rows = np.nonzero(~dele[:, 0])[0]
+            sub_frag[ins_rows, p[ins_rows, 0]] = rng.integers(0, 4, len(ins_rows))
+            frag[R] = sub_frag
+        frag = np.ascontiguousarray(frag[:, :read_len])
+        frag[strand] = (3 - frag[strand, ::-1])
+        flat = frag.reshape(-1)
+        si = rng.integers(0, flat.size, rng.binomial(flat.size, sub_rate))
+        flat[si] = (flat[si] + rng.integers(1, 4, len(si))) % 4
+        flat[rng.integers(0, flat.size, rng.binomial(flat.size, n_rate))] = 4
+        out[c0:c0 + nr] = frag
     return out, np.full(num_reads, read_len, np.int32)
 
 

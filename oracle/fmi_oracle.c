@@ -504,6 +504,14 @@ void fmi_oracle_delete(or_fmi *f) {
   }
 }
 int64_t fmi_oracle_bwt_calls(const or_fmi *f) { return f->bwt_calls; }
+/* A second handle over the same CP_OCC table (own work counter) for multi-threaded CPU runs. */
+or_fmi *fmi_oracle_share(const or_fmi *f) {
+  or_fmi *g = (or_fmi *)malloc(sizeof(or_fmi));
+  *g = *f;
+  g->bwt_calls = 0;
+  return g;
+}
+void fmi_oracle_unshare(or_fmi *g) { free(g); }
 void fmi_oracle_info(const or_fmi *f, int64_t *n, int64_t *count5, int64_t *sentinel) {
   *n = f->n;
   for (int b = 0; b < 5; b++) count5[b] = f->count[b];

@@ -25,6 +25,9 @@ def _decl(lib):
     lib.fmi_oracle_bwt_calls.argtypes = [vp]
     lib.fmi_oracle_bwt_calls.restype = i64
     lib.fmi_oracle_info.argtypes = [vp, vp, vp, vp]
+    lib.fmi_oracle_share.argtypes = [vp]
+    lib.fmi_oracle_share.restype = vp
+    lib.fmi_oracle_unshare.argtypes = [vp]
 
 
 class OracleIndex:
@@ -63,6 +66,33 @@ class OracleIndex:
                                       bc.ctypes.data, pc.ctypes.data)
         assert tot >= 0
         return out[:tot], bc, pc
+
+    def run_threaded(self, codes, lens, threads, batch_size=512, min_seed_len=19):
+        """Batches split over `threads` OS threads (ctypes releases the GIL), each with its own
+        handle over the shared CP_OCC table; returns (total SMEMs, backwardExt calls)."""
+        from concurrent.futures import ThreadPoolExecutor
+        codes = np.ascontiguousarray(codes, np.uint8)
+        lens = np.ascontiguousarray(lens, np.int32)
+        nreads, maxlen = codes.shape
+        nb = (nreads + batch_size - 1) // batch_size
+        per = (nb + threads - 1) // threads * batch_size
+
+        def work(t):
+            lo, hi = t * per, min(nreads, (t + 1) * per)
+            if lo >= hi:
+                return 0, 0
+            h = self.lib.fmi_oracle_share(self.h)
+            cap = (hi - lo) * (4 * maxlen + 16)
+            out = np.zeros(cap, SMEM_DTYPE)
+            tot = self.lib.fmi_oracle_run(h, codes[lo:hi].ctypes.data, lens[lo:hi].ctypes.data, hi - lo,
+                                          maxlen, batch_size, min_seed_len, out.ctypes.data, cap, None, None)
+            calls = self.lib.fmi_oracle_bwt_calls(h)
+            self.lib.fmi_oracle_unshare(h)
+            return tot, calls
+
+        with ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(work, range(threads)))
+        return sum(r[0] for r in res), sum(r[1] for r in res)
 
     def bwt_calls(self):
         return self.lib.fmi_oracle_bwt_calls(self.h)
