@@ -36,6 +36,10 @@ PEAK_HBM = 8.0e12                    # HBM3E spec bytes/s (MI355X_MICROARCH.md)
 FMI_BYTES_PER_EXT = 128              # 2 x 64-B CP_OCC lines per backwardExt
 
 
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -162,6 +166,7 @@ def bench_phmm(args, D, rank, world):
     from genomicsbench_palisade_amd._tc import TestcaseArray
 
     phmm.init_pairhmm()
+    log("phmm: generating + packing the job")
     batches = gen.phmm_dataset("large", args.batches, seed=1 + rank)
     ta = TestcaseArray.from_batches(batches)
     job = phmm.DeviceBatch(ta)
@@ -196,6 +201,7 @@ def bench_phmm(args, D, rank, world):
         kern, ach, peak = "phmm_forward<double>", PHMM_FLOP_PER_CELL * cells_f64 / (ms64 * 1e-3), PEAK_F64_OPS
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("phmm: CPU baseline")
         cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
     job.close()
     return {
@@ -211,10 +217,13 @@ def bench_fmi(args, D, rank, world):
     from genomicsbench_palisade_amd import fmi, gen
 
     t0 = time.perf_counter()
+    log("fmi: reference + GPU index build")
     ref = gen.fmi_reference(int(args.fmi_ref_mbp * 1e6), seed=7)  # same reference on every rank
     idx = fmi.Index.build(ref)
     t_index = time.perf_counter() - t0
+    log("fmi: generating reads")
     codes, lens = gen.fmi_reads(ref, args.fmi_reads, read_len=151, seed=8 + rank)
+    log("fmi: timed search")
     rs = fmi.Reads(idx, codes, lens)
     for _ in range(args.warmup):
         rs.search(19)
@@ -241,7 +250,9 @@ def bench_fmi(args, D, rank, world):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import fmi_util
-        oi = fmi_util.OracleIndex(ref)
+        n_, c_, s_ = idx.info()
+        oi = fmi_util.OracleIndex(adopt=(n_, c_, s_, idx.cp_occ()))  # same tables, no CPU SA build
+        log("fmi: CPU baseline")
         cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds)
         oi.close()
     n, _, _ = idx.info()

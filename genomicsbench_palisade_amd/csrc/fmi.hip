@@ -32,7 +32,9 @@
 
 namespace gbfmi {
 
-constexpr int kCap = 64;  // SMEM slots per read (7.7 on average on the synthetic sets; overflow is an error)
+constexpr int kCap = 40;       // first-pass SMEM slots per read (~8 on average on the synthetic sets)
+constexpr int kBigCap = 2048;  // second pass, for the rare reads that overflow the first
+constexpr int kMaxOvf = 16384; // reads the second pass can take
 
 struct __attribute__((aligned(16))) Ent {  // one `prev` entry (SMEM without rid)
   int64_t k, l, s;
@@ -99,11 +101,16 @@ struct SearchArgs {
   const int32_t *lens;
   int32_t nreads, stride, min_seed_len, split_len;
   Ent *scratch;          // per lane: stride entries
-  gb_smem *slots;        // per read: kCap entries
+  gb_smem *slots;        // per slot: cap entries (pass 1: slot = read, pass 2: list position)
+  int32_t cap;
+  const int32_t *list;   // pass 2: reads to redo (null in pass 1)
+  const int32_t *list_n; // pass 2: number of reads in `list`
   int32_t *counts;       // per read: total SMEMs
   int32_t *phase;        // per read: num_smem1, num_smem2, num_smem3
   int32_t *next_read;    // work counter
-  int32_t *overflow;     // reads that exceeded kCap
+  int32_t *ovf_list;     // pass 1: reads that exceeded cap (redone by pass 2)
+  int32_t *ovf_n;
+  int32_t *fatal;        // pass 2 overflow / list overflow
   unsigned long long *bwt_calls;
 };
 
@@ -115,7 +122,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
   Ent *const prev = A.scratch + (size_t)gid * A.stride;
-  unsigned long long calls = 0;
+  unsigned long long calls = 0, calls_read = 0;  // backwardExt calls (all reads / this read)
 
   int st = NEXT_READ;
   int rd = 0, L = 0, mode = 0;
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   Ent *r = prev;                   // reversed prev list: r[0] = last pushed
 
   auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
-    if (nout < kCap) {
+    if (nout < A.cap) {
       gb_smem e;
       e.rid = (uint32_t)rd;
       e.m = m;
@@ -152,22 +159,25 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     bool req = false;
     while (!req && st != DONE) {
       switch (st) {
-        case NEXT_READ:
-          rd = atomicAdd(A.next_read, 1);
-          if (rd >= A.nreads) {
+        case NEXT_READ: {
+          const int slot = atomicAdd(A.next_read, 1);
+          if (slot >= (A.list ? *A.list_n : A.nreads)) {
             st = DONE;
             break;
           }
+          rd = A.list ? A.list[slot] : slot;
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
-          o = A.slots + (size_t)rd * kCap;
+          o = A.slots + (size_t)slot * A.cap;
           nout = 0;
           ovf = false;
+          calls_read = 0;
           mode = 1;
           x = 0;
           min_intv = 1;
           st = OP_START;
           break;
+        }
         case OP_START:
           if (mode == 1 && x >= L) {  // getSMEMsAllPosOneThread done: reseed next
             n1 = nout;
@@ -275,7 +285,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           // fmi.cpp:293-302: SMEMs of length >= split_len with s <= splitWidth(10) restart at
           // the midpoint with min_intv = s + 1
           bool found = false;
-          while (ridx < n1 && ridx < kCap) {
+          while (ridx < n1 && ridx < A.cap) {
             const gb_smem e = o[ridx];
             const int start = (int)e.m, end = (int)e.n + 1;
             if (!(end - start < A.split_len || e.s > 10)) {
@@ -334,7 +344,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           req = true;
           break;
         case FINISH: {
-          const int n = nout < kCap ? nout : kCap;
+          const int n = nout < A.cap ? nout : A.cap;
           for (int i = 1; i < n; i++) {  // insertion sort by (m asc, n desc)
             const gb_smem e = o[i];
             int t = i - 1;
@@ -344,11 +354,23 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             }
             o[t + 1] = e;
           }
-          A.counts[rd] = n;
+          A.counts[rd] = nout;
           A.phase[3 * rd + 0] = n1;
           A.phase[3 * rd + 1] = n2;
           A.phase[3 * rd + 2] = nout - n1 - n2;
-          if (ovf) atomicAdd(A.overflow, 1);
+          // a read redone by pass 2 is counted there, not here
+          if (!ovf || A.list) calls += calls_read;
+          if (ovf) {
+            if (A.list) {
+              atomicAdd(A.fatal, 1);
+            } else {
+              const int k = atomicAdd(A.ovf_n, 1);
+              if (k < kMaxOvf)
+                A.ovf_list[k] = rd;
+              else
+                atomicAdd(A.fatal, 1);
+            }
+          }
           st = NEXT_READ;
           break;
         }
@@ -362,7 +384,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     // ---- one backwardExt per lane per trip --------------------------------------------------
     int64_t ko, lo, so;
     bwt_ext(F, rk, rl, rs, rb, ko, lo, so);
-    calls++;
+    calls_read++;
 
     // ---- consume ------------------------------------------------------------------------------
     if (st == FWD_NEXT) {
@@ -419,14 +441,25 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   atomicAdd(A.bwt_calls, calls);
 }
 
-__global__ void scatter_smems(const gb_smem *__restrict__ slots, const int32_t *__restrict__ counts,
+// Reads with count <= kCap are in their pass-1 slot; the rest in the pass-2 slot at the position of
+// the read in the overflow list (ovf_pos, filled by mark_overflow).
+__global__ void mark_overflow(const int32_t *__restrict__ ovf_list, const int32_t *__restrict__ ovf_n,
+                              int32_t *__restrict__ ovf_pos) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = min(*ovf_n, kMaxOvf);
+  if (t < n) ovf_pos[ovf_list[t]] = t;
+}
+
+__global__ void scatter_smems(const gb_smem *__restrict__ slots, const gb_smem *__restrict__ big,
+                              const int32_t *__restrict__ ovf_pos, const int32_t *__restrict__ counts,
                               const int64_t *__restrict__ offsets, gb_smem *__restrict__ out,
                               int32_t nreads) {
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
   if (rd >= nreads) return;
   const int n = counts[rd];
   const int64_t o = offsets[rd];
-  for (int i = 0; i < n; i++) out[o + i] = slots[(size_t)rd * kCap + i];
+  const gb_smem *src = n <= kCap ? slots + (size_t)rd * kCap : big + (size_t)ovf_pos[rd] * kBigCap;
+  for (int i = 0; i < n; i++) out[o + i] = src[i];
 }
 
 }  // namespace gbfmi
@@ -449,7 +482,10 @@ struct gb_fmi_reads {
   int64_t *d_offsets = nullptr;
   gb_smem *d_out = nullptr;
   int64_t out_cap = 0;
-  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow
+  int32_t *d_ctl = nullptr;  // [0] next_read pass 1, [1] overflow count, [2] fatal, [3] next_read pass 2
+  int32_t *d_ovf_list = nullptr;
+  int32_t *d_ovf_pos = nullptr;
+  gb_smem *d_big = nullptr;
   unsigned long long *d_calls = nullptr;
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
@@ -566,11 +602,14 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   if (e == hipSuccess) e = hipMalloc(&R->d_lens, nr * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&R->d_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::Ent));
   if (e == hipSuccess) e = hipMalloc(&R->d_slots, nr * gbfmi::kCap * sizeof(gb_smem));
+  if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_ovf_pos, nr * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&R->d_big, (size_t)gbfmi::kMaxOvf * gbfmi::kBigCap * sizeof(gb_smem));
   if (e == hipSuccess) e = hipMalloc(&R->d_counts, nr * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&R->d_phase, nr * 3 * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&R->d_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 4 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_calls, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&R->d_calls, 2 * sizeof(unsigned long long));
   if (e == hipSuccess)
     e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
   if (e == hipSuccess) e = hipMalloc(&R->d_temp, std::max<size_t>(R->temp_bytes, 16));
@@ -590,7 +629,8 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   if (R->stream) (void)hipStreamSynchronize(R->stream);
   for (void *p : {(void *)R->d_qdb, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
-                  (void *)R->d_ctl, (void *)R->d_calls, R->d_temp})
+                  (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
+                  (void *)R->d_ovf_pos, (void *)R->d_big})
     (void)hipFree(p);
   for (auto ev : R->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -605,7 +645,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   GB_HIP(hipSetDevice(R->idx->device));
   GB_HIP(hipEventRecord(R->ev[0], R->stream));
   GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
-  GB_HIP(hipMemsetAsync(R->d_calls, 0, sizeof(unsigned long long), R->stream));
+  GB_HIP(hipMemsetAsync(R->d_calls, 0, 2 * sizeof(unsigned long long), R->stream));
   gbfmi::SearchArgs A;
   A.F.occ = R->idx->d_occ;
   for (int b = 0; b < 5; b++) A.F.count[b] = R->idx->count[b];
@@ -621,11 +661,31 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   A.counts = R->d_counts;
   A.phase = R->d_phase;
   A.next_read = R->d_ctl;
-  A.overflow = R->d_ctl + 1;
+  A.ovf_list = R->d_ovf_list;
+  A.ovf_n = R->d_ctl + 1;
+  A.fatal = R->d_ctl + 2;
   A.bwt_calls = R->d_calls;
   if (R->nreads > 0) {
+    // pass 1: every read, kCap slots each
+    A.slots = R->d_slots;
+    A.cap = gbfmi::kCap;
+    A.list = nullptr;
+    A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
     hipLaunchKernelGGL(gbfmi::smem_search, dim3(blocks), dim3(64), 0, R->stream, A);
+    GB_HIP(hipGetLastError());
+    // pass 2: the reads that overflowed (usually none), kBigCap slots each; the read count stays
+    // on the device, idle lanes exit at once
+    A.slots = R->d_big;
+    A.cap = gbfmi::kBigCap;
+    A.list = R->d_ovf_list;
+    A.list_n = R->d_ctl + 1;
+    A.next_read = R->d_ctl + 3;
+    A.bwt_calls = R->d_calls;
+    hipLaunchKernelGGL(gbfmi::smem_search, dim3(32), dim3(64), 0, R->stream, A);
+    GB_HIP(hipGetLastError());
+    hipLaunchKernelGGL(gbfmi::mark_overflow, dim3((gbfmi::kMaxOvf + 255) / 256), dim3(256), 0, R->stream,
+                       R->d_ovf_list, R->d_ctl + 1, R->d_ovf_pos);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(R->ev[1], R->stream));
@@ -652,8 +712,9 @@ int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t ou
   GB_HIP(hipStreamSynchronize(R->stream));
   int32_t ctl[4];
   GB_HIP(hipMemcpy(ctl, R->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
-  if (ctl[1] != 0) {
-    gb::set_error("gb_fmi_results: %d reads exceeded %d SMEM slots", ctl[1], gbfmi::kCap);
+  if (ctl[2] != 0) {
+    gb::set_error("gb_fmi_results: %d reads exceeded %d SMEM slots (or more than %d reads exceeded %d)",
+                  ctl[2], gbfmi::kBigCap, gbfmi::kMaxOvf, gbfmi::kCap);
     return GB_ERR_STATE;
   }
   const int32_t n = R->nreads;
@@ -687,7 +748,7 @@ int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t ou
     }
     if (tot) {
       hipLaunchKernelGGL(gbfmi::scatter_smems, dim3((n + 255) / 256), dim3(256), 0, R->stream,
-                         R->d_slots, R->d_counts, R->d_offsets, R->d_out, n);
+                         R->d_slots, R->d_big, R->d_ovf_pos, R->d_counts, R->d_offsets, R->d_out, n);
       GB_HIP(hipGetLastError());
       GB_HIP(hipMemcpyAsync(out, R->d_out, sizeof(gb_smem) * (size_t)tot, hipMemcpyDeviceToHost, R->stream));
       GB_HIP(hipStreamSynchronize(R->stream));

@@ -212,6 +212,21 @@ int fmi_oracle_load(const char *path, or_fmi *idx) {
   return 0;
 }
 
+/* Adopt tables produced elsewhere (e.g. the product's GPU builder, whose output is tested
+ * bit-identical to fmi_oracle_build's): count5 as stored in the file (before the +1). The caller keeps
+ * cp_occ alive; fmi_oracle_free must not be called on such a handle. */
+void fmi_oracle_adopt(or_fmi *idx, int64_t n, const int64_t *count5_file, int64_t sentinel, void *cp_occ) {
+  idx->n = n;
+  for (int b = 0; b < 5; b++) idx->count[b] = count5_file[b] + 1;
+  idx->sentinel_index = sentinel;
+  idx->cp_occ = (or_cp_occ *)cp_occ;
+  idx->cp_occ_size = (n >> CP_SHIFT) + 1;
+  idx->bwt_calls = 0;
+  idx->one_hot_mask[0] = 0;
+  idx->one_hot_mask[1] = 0x8000000000000000ull;
+  for (int i = 2; i < 64; i++) idx->one_hot_mask[i] = (idx->one_hot_mask[i - 1] >> 1) | 0x8000000000000000ull;
+}
+
 void fmi_oracle_free(or_fmi *idx) {
   free(idx->cp_occ);
   idx->cp_occ = NULL;
@@ -442,7 +457,7 @@ int64_t fmi_oracle_run(or_fmi *f, const uint8_t *enc_qdb, const int32_t *lens, i
   int16_t *qpos = (int16_t *)malloc((size_t)batch_size * 64 * sizeof(int16_t));
   int32_t *cum = (int32_t *)malloc((size_t)batch_size * sizeof(int32_t));
   or_smem *prev = (or_smem *)malloc((size_t)(max_readlength + 1) * sizeof(or_smem));
-  const int64_t per_batch_cap = (int64_t)batch_size * (2 * max_readlength + 8);
+  const int64_t per_batch_cap = (int64_t)batch_size * (8 * (int64_t)max_readlength + 64);
   or_smem *tmp = (or_smem *)malloc((size_t)per_batch_cap * sizeof(or_smem));
   int64_t total = 0;
   for (int32_t i = 0; i < numReads; i += batch_size) {

@@ -30,7 +30,7 @@
 #define OR_JAC_TOL 8.0
 #define OR_JAC_STEP 0.0001
 #define OR_JAC_INV_STEP (1.0 / OR_JAC_STEP)
-#define OR_JAC_SIZE ((int)(OR_JAC_TOL / OR_JAC_STEP) + 1)
+#define OR_JAC_SIZE 80001 /* JACOBIAN_LOG_TABLE_SIZE = (int)(8.0 / 0.0001) + 1 (Context.h:10) */
 #define OR_M2M_SIZE (((OR_MAX_QUAL + 1) * (OR_MAX_QUAL + 2)) >> 1)
 
 typedef struct {

@@ -25,18 +25,26 @@ def _decl(lib):
     lib.fmi_oracle_bwt_calls.argtypes = [vp]
     lib.fmi_oracle_bwt_calls.restype = i64
     lib.fmi_oracle_info.argtypes = [vp, vp, vp, vp]
+    lib.fmi_oracle_adopt.argtypes = [vp, i64, vp, i64, vp]
     lib.fmi_oracle_share.argtypes = [vp]
     lib.fmi_oracle_share.restype = vp
     lib.fmi_oracle_unshare.argtypes = [vp]
 
 
 class OracleIndex:
-    def __init__(self, ref_codes=None, path_out=None, load_path=None):
+    def __init__(self, ref_codes=None, path_out=None, load_path=None, adopt=None):
         self.lib = oracle_lib.oracle()
         if not getattr(self.lib, "_fmi_decl", False):
             _decl(self.lib)
             self.lib._fmi_decl = True
         self.h = self.lib.fmi_oracle_new()
+        if adopt is not None:  # (n, count5_after_load, sentinel, cp_occ int64[rows, 8])
+            n, count5, sentinel, occ = adopt
+            self._occ = np.ascontiguousarray(occ)
+            c = np.array([x - 1 for x in count5], np.int64)
+            self.lib.fmi_oracle_adopt(self.h, n, c.ctypes.data, sentinel, self._occ.ctypes.data)
+            self._adopted = True
+            return
         if load_path is not None:
             st = self.lib.fmi_oracle_load(load_path.encode(), self.h)
         else:
@@ -56,7 +64,7 @@ class OracleIndex:
         codes = np.ascontiguousarray(codes, np.uint8)
         lens = np.ascontiguousarray(lens, np.int32)
         nreads, maxlen = codes.shape
-        cap = nreads * (4 * maxlen + 16)
+        cap = nreads * (8 * maxlen + 64)
         out = np.zeros(cap, SMEM_DTYPE)
         nb = (nreads + batch_size - 1) // batch_size
         bc = np.zeros(nb, np.int64)
@@ -82,7 +90,7 @@ class OracleIndex:
             if lo >= hi:
                 return 0, 0
             h = self.lib.fmi_oracle_share(self.h)
-            cap = (hi - lo) * (4 * maxlen + 16)
+            cap = (hi - lo) * (8 * maxlen + 64)
             out = np.zeros(cap, SMEM_DTYPE)
             tot = self.lib.fmi_oracle_run(h, codes[lo:hi].ctypes.data, lens[lo:hi].ctypes.data, hi - lo,
                                           maxlen, batch_size, min_seed_len, out.ctypes.data, cap, None, None)
@@ -99,7 +107,10 @@ class OracleIndex:
 
     def close(self):
         if self.h:
-            self.lib.fmi_oracle_delete(self.h)
+            if getattr(self, "_adopted", False):
+                self.lib.fmi_oracle_unshare(self.h)  # tables belong to self._occ
+            else:
+                self.lib.fmi_oracle_delete(self.h)
             self.h = None
 
 

@@ -103,3 +103,21 @@ def test_empty_and_degenerate_reads(fmi):
     rs.search(19)
     sm, tot, _, _ = rs.results(batch_size=4)
     assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
+
+
+def test_overflow_second_pass(fmi):
+    """Short min_seed_len gives far more SMEMs per read than the first-pass slots (40): those reads
+    are redone by the second pass and must still match the oracle exactly."""
+    ref = gen.fmi_reference(400_000, seed=31, repeat_frac=0.3)
+    codes, lens = gen.fmi_reads(ref, 1500, read_len=151, seed=32, sub_rate=0.08)
+    oi = fmi_util.OracleIndex(ref)
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512, min_seed_len=6)
+    per_read = np.bincount(exp["rid"], minlength=len(lens))
+    assert per_read.max() > 40, per_read.max()
+    idx = fmi.Index.build(ref)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(6)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
+    assert (bc == ebc).all() and (pc == epc).all()
+    assert rs.timing()[2] == oi.bwt_calls()
