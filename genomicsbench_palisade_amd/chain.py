@@ -1,0 +1,64 @@
+"""Host mirror of the reference chaining interface (host_chain_kernel, benchmarks/chain/src/
+host_kernel.cpp:481-501) over CSR call sets (gen.ChainCalls), executed by csrc/chain.hip."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import check, lib
+
+
+def _decl():
+    L = lib()
+    if getattr(L, "_chain_decl", False):
+        return L
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    L.gb_chain_batch_create.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.POINTER(vp)]
+    L.gb_chain_batch_run.argtypes = [vp]
+    L.gb_chain_batch_sync.argtypes = [vp]
+    L.gb_chain_batch_results.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.gb_chain_batch_timing.argtypes = [vp, vp]
+    L.gb_chain_batch_destroy.argtypes = [vp]
+    L._chain_decl = True
+    return L
+
+
+class ChainBatch:
+    def __init__(self, calls):
+        L = _decl()
+        self.calls = calls
+        self.h = ctypes.c_void_p()
+        check(L.gb_chain_batch_create(calls.ncalls, calls.offsets.ctypes.data, calls.avg_qspan.ctypes.data,
+                                      calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data,
+                                      ctypes.byref(self.h)), "gb_chain_batch_create")
+
+    def run(self):
+        check(_decl().gb_chain_batch_run(self.h), "gb_chain_batch_run")
+
+    def sync(self):
+        check(_decl().gb_chain_batch_sync(self.h), "gb_chain_batch_sync")
+
+    def results(self):
+        n = self.calls.nanchors
+        out = [np.zeros(max(n, 1), np.int32) for _ in range(4)]
+        v = ctypes.c_int64()
+        check(_decl().gb_chain_batch_results(self.h, *[o.ctypes.data for o in out], ctypes.byref(v)),
+              "gb_chain_batch_results")
+        return [o[:n] for o in out] + [v.value]
+
+    def timing(self):
+        ms = ctypes.c_float()
+        check(_decl().gb_chain_batch_timing(self.h, ctypes.byref(ms)), "gb_chain_batch_timing")
+        return ms.value
+
+    def close(self):
+        if self.h:
+            _decl().gb_chain_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

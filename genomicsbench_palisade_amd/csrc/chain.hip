@@ -1,0 +1,366 @@
+// chain.hip -- MI355X (gfx950) minimap2 chaining DP (chain_dp): kernel and C ABI.
+//
+// Semantics: benchmarks/chain/src/host_kernel.cpp:405-472 (plaintext branch) ==
+// tools/minimap2-acceleration/kernel/scalar/src/host_kernel.cpp:30-94, with the C integer / double
+// semantics of that source (int64 dr, int32 truncations, (int)(dd * .01 * avg_qspan), no FMA).
+//
+// MI355X design: one call (read) per wave64; anchors are processed in order i (score[i] depends on
+// score[j < i]) and the predecessor loop j = i-1 .. st runs 64 candidates per step, lane l taking
+// j = jtop - l, i.e. lanes in the reference's visiting order. The reference loop is sequential only
+// through three quantities, each turned into a wave-wide prefix scan:
+//   max_f        running maximum of the candidate scores             (max scan)
+//   n_skip       max(n-1, 0) on an improvement, n+1 on a "targeted" non-improvement
+//                -> compositions of n -> max(n + a, b), closed under composition (pair scan)
+//   break        first lane where n_skip exceeds 25                   (ballot + ctz)
+// "targets[j] == i" is decided by marks from earlier-visited j' (> j) of the same i, which are all
+// visited before any break that could stop j: marks are i+1 stamps in an LDS ring indexed by j.
+// The last 64 anchors (the first step of every i) live in registers, shifted one lane per i with
+// DPP, so most anchors need no memory access at all; older candidates are read from global memory
+// through L2 (sc1 loads) after a periodic vmcnt drain that orders the wave's own stores before them.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <numeric>
+#include <vector>
+
+#include "../../include/gb_chain.h"
+#include "gb_common.h"
+
+namespace gbchain {
+
+constexpr int kRing = 8192;     // stamp ring >= max_iter (5000) + 64 candidates
+constexpr int kMaxIter = 5000;  // host_kernel.cpp:41
+constexpr int kMaxSkip = 25;    // host_kernel.cpp:42
+
+struct Args {
+  const int64_t *offsets;
+  const float *avg_qspan;
+  const int32_t *params4;
+  const uint64_t *x, *y;
+  const int32_t *order;  // calls, longest first
+  int32_t *score, *parent, *target, *peak;
+  unsigned long long *visited;
+};
+
+__device__ __forceinline__ int ilog2_32(uint32_t v) { return 31 - __clz((int)v); }  // v > 0 (LogTable256)
+
+__device__ __forceinline__ int dpp_shr_i32(int v, int lane0) {
+  return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+__device__ __forceinline__ uint64_t dpp_shr_u64(uint64_t v, uint64_t lane0) {
+  const int lo = dpp_shr_i32((int)(uint32_t)v, (int)(uint32_t)lane0);
+  const int hi = dpp_shr_i32((int)(uint32_t)(v >> 32), (int)(uint32_t)(lane0 >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ int32_t load_l2(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1 (bypasses L1)
+}
+
+__global__ __launch_bounds__(64) void chain_kernel(Args A) {
+  __shared__ uint32_t S[kRing];
+  const int c = A.order[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int64_t o = A.offsets[c];
+  const int64_t n = A.offsets[c + 1] - o;
+  const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
+  const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
+  const double avg_qspan = (double)A.avg_qspan[c];
+  const uint64_t *X = A.x + o, *Y = A.y + o;
+  int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
+
+  for (int k = lane; k < kRing; k += 64) S[k] = 0;
+  for (int64_t k = lane; k < n; k += 64) target[k] = 0;  // a fresh std::vector in the reference
+  __builtin_amdgcn_s_waitcnt(0);  // zeroing stores complete before any later targets store
+  __syncthreads();
+
+  // register window: lane l holds anchor i-1-l
+  uint64_t wx = 0, wy = 0;
+  int32_t ws = 0, wpar = -1, wpk = 0;
+  uint64_t px = 0, py = 0;  // anchor i-1
+  int32_t ps = 0, pp = -1, pk = 0;
+  int64_t st = 0;
+  unsigned long long vis = 0;
+
+  for (int64_t i = 0; i < n; i++) {
+    if (i > 0) {
+      wx = dpp_shr_u64(wx, px);
+      wy = dpp_shr_u64(wy, py);
+      ws = dpp_shr_i32(ws, ps);
+      wpar = dpp_shr_i32(wpar, pp);
+      wpk = dpp_shr_i32(wpk, pk);
+    }
+    if ((i & 31) == 0) __builtin_amdgcn_s_waitcnt(0);  // stores of steps <= i-32 are in L2
+    const uint64_t xi = X[i], yi = Y[i];
+    const int32_t qi = (int32_t)yi, q_span = (int32_t)(yi >> 32 & 0xff);
+    const int32_t sidi = (int32_t)((yi & (0xffull << 48)) >> 48);
+    while (st < i && xi > X[st] + (uint64_t)(int64_t)max_dist_x) ++st;
+    if (i - st > kMaxIter) st = i - kMaxIter;
+
+    int32_t M = q_span, N = 0;
+    int64_t J = -1;
+    const uint32_t stamp = (uint32_t)(i + 1);
+    for (int64_t jtop = i - 1; jtop >= st; jtop -= 64) {
+      const int64_t j = jtop - lane;
+      const bool valid = j >= st;
+      uint64_t xj, yj;
+      int32_t scj, pj;
+      if (jtop == i - 1) {
+        xj = wx;
+        yj = wy;
+        scj = ws;
+        pj = wpar;
+      } else if (valid) {
+        xj = X[j];
+        yj = Y[j];
+        scj = load_l2(score + j);
+        pj = load_l2(parent + j);
+      } else {
+        xj = yj = 0;
+        scj = 0;
+        pj = -1;
+      }
+      // ---- candidate score (host_kernel.cpp:55-82), lane-parallel ---------------------------
+      bool ok = valid;
+      int32_t sc = INT_MIN;
+      if (ok) {
+        const int64_t dr = (int64_t)(xi - xj);
+        const int32_t dq = qi - (int32_t)yj;
+        const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
+        if ((sidi == sidj && dr == 0) || dq <= 0) ok = false;
+        if ((sidi == sidj && dq > max_dist_y) || dq > max_dist_x) ok = false;
+        const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
+        if (sidi == sidj && dd > bw) ok = false;
+        if (n_segs > 1 && sidi == sidj && dr > max_dist_y) ok = false;  // is_cdna = 0
+        if (ok) {
+          const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
+          int32_t s = (int32_t)(min_d > q_span ? (int64_t)q_span : (dq < dr ? (int64_t)dq : dr));
+          const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
+          int gap_cost = 0;
+          if (sidi != sidj) {
+            const int c_lin = (int)((double)dd * .01 * avg_qspan), c_log = log_dd;
+            if (dr == 0)
+              ++s;
+            else
+              gap_cost = c_lin < c_log ? c_lin : c_log;
+          } else {
+            gap_cost = (int)((double)dd * .01 * avg_qspan) + (log_dd >> 1);
+          }
+          s -= (int)((double)gap_cost * (double)1.0f + .499);
+          sc = s + scj;
+        }
+      }
+      // ---- "targets[j] == i": stamps from visited j' > j with parents[j'] == j --------------
+      if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
+      const bool tgt = valid && S[j & (kRing - 1)] == stamp;
+      // ---- sequential order as prefix scans over lanes ---------------------------------------
+      int32_t mx = ok ? sc : INT_MIN;  // inclusive max scan
+      int32_t a = 0, b = 0;            // n -> max(n + a, b)
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t u = __shfl_up(mx, d);
+        if (lane >= d) mx = max(mx, u);
+      }
+      int32_t before = __shfl_up(mx, 1);
+      if (lane == 0) before = INT_MIN;
+      before = max(before, M);
+      const bool upd = ok && sc > before;
+      a = upd ? -1 : ((ok && tgt) ? 1 : 0);
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t ua = __shfl_up(a, d), ub = __shfl_up(b, d);
+        if (lane >= d) {
+          const int32_t na = ua + a, nb = max(ub + a, b);
+          a = na;
+          b = nb;
+        }
+      }
+      const int32_t n_after = max(N + a, b);
+      const bool brk = ok && !upd && tgt && n_after > kMaxSkip;
+      const uint64_t bm = __ballot(brk);
+      const int bl = bm ? __builtin_ctzll(bm) : 64;
+      const int64_t nvalid = min((int64_t)64, jtop - st + 1);
+      vis += (bl < 64) ? (unsigned long long)(bl + 1) : (unsigned long long)nvalid;
+      // processed lanes l < bl: max_f, max_j, targets
+      const uint64_t low = bl >= 64 ? ~0ull : ((1ull << bl) - 1);
+      const uint64_t um = __ballot(upd) & low;
+      if (um) {
+        const int lu = 63 - __builtin_clzll(um);
+        J = jtop - lu;
+        M = __shfl(mx, lu);
+      }
+      if (ok && lane < bl && pj >= 0) target[pj] = (int32_t)i;
+      if (bl < 64) break;
+      N = __shfl(n_after, 63);
+    }
+    int32_t pkJ = 0;
+    if (J >= 0) pkJ = (J >= i - 64) ? __shfl(wpk, (int)(i - 1 - J)) : load_l2(peak + J);
+    const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
+    if (lane == 0) {
+      score[i] = M;
+      parent[i] = (int32_t)J;
+      peak[i] = pki;
+    }
+    px = xi;
+    py = yi;
+    ps = M;
+    pp = (int32_t)J;
+    pk = pki;
+  }
+  // wave-reduce the visited count
+  for (int d = 32; d >= 1; d >>= 1) vis += __shfl_xor(vis, d);
+  if (lane == 0) atomicAdd(A.visited, vis / 64);
+}
+
+}  // namespace gbchain
+
+struct gb_chain_batch {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int64_t ncalls = 0, nanchors = 0;
+  int64_t *d_off = nullptr;
+  float *d_aq = nullptr;
+  int32_t *d_par4 = nullptr, *d_order = nullptr;
+  uint64_t *d_x = nullptr, *d_y = nullptr;
+  int32_t *d_out = nullptr;  // score | parent | target | peak
+  unsigned long long *d_vis = nullptr;
+  bool ran = false;
+};
+
+extern "C" {
+
+int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
+                          const int32_t *params4, const uint64_t *x, const uint64_t *y,
+                          gb_chain_batch **out) {
+  GB_ARG(out && ncalls >= 0 && offsets, "gb_chain_batch_create: bad arguments");
+  GB_ARG(ncalls < (1ll << 31), "gb_chain_batch_create: too many calls");
+  *out = nullptr;
+  const int64_t na = offsets[ncalls];
+  GB_ARG(offsets[0] == 0 && na >= 0 && (na == 0 || (x && y)), "gb_chain_batch_create: bad offsets");
+  for (int64_t c = 0; c < ncalls; c++)
+    GB_ARG(offsets[c + 1] >= offsets[c] && offsets[c + 1] - offsets[c] < (1ll << 31),
+           "gb_chain_batch_create: call %lld has a bad anchor range", (long long)c);
+  GB_ARG(ncalls == 0 || (avg_qspan && params4), "gb_chain_batch_create: null parameters");
+  // longest calls first: the grid is dispatched in order, so the critical path starts first
+  std::vector<int32_t> order((size_t)ncalls);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return offsets[a + 1] - offsets[a] > offsets[b + 1] - offsets[b];
+  });
+  auto *B = new gb_chain_batch();
+  B->ncalls = ncalls;
+  B->nanchors = na;
+  hipError_t e = hipGetDevice(&B->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
+  for (auto &ev : B->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  const size_t nc = (size_t)std::max<int64_t>(ncalls, 1), nn = (size_t)std::max<int64_t>(na, 1);
+  if (e == hipSuccess) e = hipMalloc(&B->d_off, (nc + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_aq, nc * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&B->d_par4, nc * 4 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_order, nc * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_x, nn * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_y, nn * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_out, nn * 4 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_vis, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpy(B->d_off, offsets, (size_t)(ncalls + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_aq, avg_qspan, (size_t)ncalls * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_par4, params4, (size_t)ncalls * 16, hipMemcpyHostToDevice);
+  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_order, order.data(), (size_t)ncalls * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && na) e = hipMemcpy(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess && na) e = hipMemcpy(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    gb::set_error("gb_chain_batch_create: %s", hipGetErrorString(e));
+    gb_chain_batch_destroy(B);
+    return GB_ERR_HIP;
+  }
+  *out = B;
+  return GB_OK;
+}
+
+int gb_chain_batch_run(gb_chain_batch *B) {
+  GB_ARG(B, "gb_chain_batch_run: null batch");
+  GB_HIP(hipSetDevice(B->device));
+  GB_HIP(hipMemsetAsync(B->d_vis, 0, sizeof(unsigned long long), B->stream));
+  GB_HIP(hipEventRecord(B->ev[0], B->stream));
+  if (B->ncalls > 0) {
+    gbchain::Args A;
+    A.offsets = B->d_off;
+    A.avg_qspan = B->d_aq;
+    A.params4 = B->d_par4;
+    A.x = B->d_x;
+    A.y = B->d_y;
+    A.order = B->d_order;
+    const size_t nn = (size_t)std::max<int64_t>(B->nanchors, 1);
+    A.score = B->d_out;
+    A.parent = B->d_out + nn;
+    A.target = B->d_out + 2 * nn;
+    A.peak = B->d_out + 3 * nn;
+    A.visited = B->d_vis;
+    hipLaunchKernelGGL(gbchain::chain_kernel, dim3((unsigned)B->ncalls), dim3(64), 0, B->stream, A);
+    GB_HIP(hipGetLastError());
+  }
+  GB_HIP(hipEventRecord(B->ev[1], B->stream));
+  B->ran = true;
+  return GB_OK;
+}
+
+int gb_chain_batch_sync(gb_chain_batch *B) {
+  GB_ARG(B, "gb_chain_batch_sync: null batch");
+  GB_HIP(hipStreamSynchronize(B->stream));
+  return GB_OK;
+}
+
+int gb_chain_batch_results(gb_chain_batch *B, int32_t *scores, int32_t *parents, int32_t *targets,
+                           int32_t *peak_scores, int64_t *visited) {
+  GB_ARG(B && B->ran, "gb_chain_batch_results: batch has not run");
+  GB_HIP(hipSetDevice(B->device));
+  GB_HIP(hipStreamSynchronize(B->stream));
+  const size_t na = (size_t)B->nanchors, nn = (size_t)std::max<int64_t>(B->nanchors, 1);
+  int32_t *dst[4] = {scores, parents, targets, peak_scores};
+  for (int k = 0; k < 4; k++)
+    if (dst[k] && na) GB_HIP(hipMemcpy(dst[k], B->d_out + k * nn, na * 4, hipMemcpyDeviceToHost));
+  if (visited) {
+    unsigned long long v = 0;
+    GB_HIP(hipMemcpy(&v, B->d_vis, sizeof(v), hipMemcpyDeviceToHost));
+    *visited = (int64_t)v;
+  }
+  return GB_OK;
+}
+
+int gb_chain_batch_timing(gb_chain_batch *B, float *kernel_ms) {
+  GB_ARG(B && B->ran, "gb_chain_batch_timing: batch has not run");
+  GB_HIP(hipEventSynchronize(B->ev[1]));
+  float ms = 0;
+  GB_HIP(hipEventElapsedTime(&ms, B->ev[0], B->ev[1]));
+  if (kernel_ms) *kernel_ms = ms;
+  return GB_OK;
+}
+
+int gb_chain_batch_destroy(gb_chain_batch *B) {
+  if (!B) return GB_OK;
+  if (B->stream) (void)hipStreamSynchronize(B->stream);
+  for (void *p : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order, (void *)B->d_x,
+                  (void *)B->d_y, (void *)B->d_out, (void *)B->d_vis})
+    (void)hipFree(p);
+  for (auto ev : B->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (B->stream) (void)hipStreamDestroy(B->stream);
+  delete B;
+  return GB_OK;
+}
+
+int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
+             const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents, int32_t *targets,
+             int32_t *peak_scores) {
+  gb_chain_batch *B = nullptr;
+  int st = gb_chain_batch_create(ncalls, offsets, avg_qspan, params4, x, y, &B);
+  if (st) return st;
+  st = gb_chain_batch_run(B);
+  if (!st) st = gb_chain_batch_results(B, scores, parents, targets, peak_scores, nullptr);
+  gb_chain_batch_destroy(B);
+  return st;
+}
+
+}  // extern "C"

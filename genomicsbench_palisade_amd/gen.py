@@ -194,3 +194,90 @@ def read_pac(path):
     b = raw[: (seq_len + 3) // 4]
     codes = np.stack([(b >> 6) & 3, (b >> 4) & 3, (b >> 2) & 3, b & 3], axis=1).reshape(-1)
     return codes[:seq_len].astype(np.uint8)
+
+
+# ---------------------------------------------------------------------------------------------
+# chain: minimap2-style anchor sets (n ~ lognormal, max 87 271 anchors per call,
+# anchors sorted by x, ~85% forward strand, spans {15,19,28}, max_dist 5000, bw 500, n_segs 1;
+# 'large' = 10 000 calls, 'small' = 1 000; seed 5)
+# ---------------------------------------------------------------------------------------------
+class ChainCalls:
+    """CSR anchor sets: anchors of call c are x[offsets[c]:offsets[c+1]] (call_t, host_data.h:19-39)."""
+
+    def __init__(self, offsets, x, y, avg_qspan, params4):
+        self.offsets = np.asarray(offsets, np.int64)
+        self.x = np.asarray(x, np.uint64)
+        self.y = np.asarray(y, np.uint64)
+        self.avg_qspan = np.asarray(avg_qspan, np.float32)
+        self.params4 = np.asarray(params4, np.int32).reshape(-1, 4)  # max_dist_x, max_dist_y, bw, n_segs
+
+    @property
+    def ncalls(self):
+        return len(self.offsets) - 1
+
+    @property
+    def nanchors(self):
+        return int(self.offsets[-1])
+
+
+def chain_call(rng, n: int):
+    """One read's anchors: a collinear true locus (~85% of anchors, with small indel drift) plus
+    spurious hits at other loci (repeats), mixed strands, sorted by x like minimap2's dumps."""
+    n_true = max(1, int(n * rng.uniform(0.75, 0.95)))
+    n_sp = n - n_true
+    spans = rng.choice(np.array([15, 19, 28]), size=n)
+    Lq = int(n_true * rng.uniform(6, 14)) + 100
+    rid0, rev0 = int(rng.integers(0, 24)), int(rng.random() < 0.15)
+    r0 = int(rng.integers(1_000_000, 200_000_000))
+    qpos = np.sort(rng.integers(0, Lq, n_true))
+    drift = np.cumsum(rng.choice(np.array([-2, -1, 0, 0, 0, 0, 1, 2]), size=n_true) *
+                      (rng.random(n_true) < 0.1))
+    rpos = r0 + qpos + drift
+    xs = [(rev0 << 63) | (rid0 << 32) | rpos.astype(np.uint64)]
+    ys = [qpos]
+    if n_sp:
+        nl = max(1, n_sp // int(rng.integers(5, 60)))
+        loc = rng.integers(0, nl, n_sp)
+        lrid = rng.integers(0, 24, nl)
+        lrev = (rng.random(nl) < 0.3).astype(np.uint64)
+        lr0 = rng.integers(1_000_000, 200_000_000, nl)
+        q = rng.integers(0, Lq, n_sp)
+        rp = lr0[loc] + q + rng.integers(-50, 50, n_sp)
+        xs.append((lrev[loc] << np.uint64(63)) | (lrid[loc].astype(np.uint64) << np.uint64(32)) | rp.astype(np.uint64))
+        ys.append(q)
+    x = np.concatenate([np.asarray(a, np.uint64) for a in xs])
+    q = np.concatenate(ys).astype(np.uint64)
+    y = (spans.astype(np.uint64) << np.uint64(32)) | q  # seg id 0
+    order = np.lexsort((y, x))
+    return x[order], y[order], float(spans.mean())
+
+
+def chain_dataset(kind: str = "large", num_calls: int | None = None, seed: int = 5,
+                  median_n: int = 1500, max_n: int = 87271):
+    rng = np.random.default_rng(seed)
+    if num_calls is None:
+        num_calls = 10_000 if kind == "large" else 1_000
+    ns = np.minimum(max_n, np.maximum(2, rng.lognormal(np.log(median_n), 1.0, num_calls).astype(np.int64)))
+    ns[int(rng.integers(0, num_calls))] = max_n  # the logged maximum (scripts/chain_small_outt:3938)
+    offs = np.zeros(num_calls + 1, np.int64)
+    xs, ys, aq = [], [], []
+    for c in range(num_calls):
+        x, y, a = chain_call(rng, int(ns[c]))
+        xs.append(x)
+        ys.append(y)
+        aq.append(a)
+        offs[c + 1] = offs[c] + len(x)
+    params = np.tile(np.array([5000, 5000, 500, 1], np.int32), (num_calls, 1))
+    return ChainCalls(offs, np.concatenate(xs), np.concatenate(ys), np.array(aq, np.float32), params)
+
+
+def write_chain_file(path, calls: ChainCalls):
+    """read_call format (benchmarks/chain/src/host_data_io.cpp:40-80)."""
+    with open(path, "w") as f:
+        for c in range(calls.ncalls):
+            o0, o1 = calls.offsets[c], calls.offsets[c + 1]
+            p = calls.params4[c]
+            f.write(f"{o1 - o0}\t{calls.avg_qspan[c]:f}\t{p[0]}\t{p[1]}\t{p[2]}\t{p[3]}\n")
+            for xx, yy in zip(calls.x[o0:o1].tolist(), calls.y[o0:o1].tolist()):
+                f.write(f"{xx}\t{yy}\n")
+            f.write("EOR\n")

@@ -1,0 +1,48 @@
+/*
+ * gb_chain.h -- C ABI of the MI355X minimap2 anchor-chaining DP (drop-in boundary for benchmarks/chain).
+ *
+ * Reference interface this replaces (paths relative to the reference repo):
+ *   void host_chain_kernel(std::vector<call_t>&, std::vector<return_t>&, int numThreads);
+ *        benchmarks/chain/src/host_kernel.h:6, host_kernel.cpp:481-501 -> chain_dp :58-479 (plaintext
+ *        branch :405-472 == tools/minimap2-acceleration/kernel/scalar/src/host_kernel.cpp:30-94)
+ *   call_t / return_t / anchor_t: benchmarks/chain/src/host_data.h:19-46
+ * The calls are flattened to CSR: anchors of call c are x[offsets[c] .. offsets[c+1]), same for y and
+ * for the four outputs. params4[4c..4c+3] = {max_dist_x, max_dist_y, bw, n_segs}.
+ * 0 on success, negative gb_status on failure (gb_last_error()).
+ */
+#ifndef GB_CHAIN_H
+#define GB_CHAIN_H
+
+#include <stdint.h>
+
+#include "gb.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gb_chain_batch gb_chain_batch;
+
+/* Upload a set of calls (anchors sorted by x within each call, as minimap2 produces them). */
+int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
+                          const int32_t *params4, const uint64_t *x, const uint64_t *y,
+                          gb_chain_batch **out);
+/* chain_dp for every call (asynchronous on the batch's stream). */
+int gb_chain_batch_run(gb_chain_batch *b);
+int gb_chain_batch_sync(gb_chain_batch *b);
+/* scores/parents/targets/peak_scores per anchor (any may be NULL); visited = total (i, j) pairs the
+ * reference loop visits (work accounting). */
+int gb_chain_batch_results(gb_chain_batch *b, int32_t *scores, int32_t *parents, int32_t *targets,
+                           int32_t *peak_scores, int64_t *visited);
+int gb_chain_batch_timing(gb_chain_batch *b, float *kernel_ms);
+int gb_chain_batch_destroy(gb_chain_batch *b);
+
+/* One-shot form of host_chain_kernel over CSR arrays. */
+int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
+             const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents,
+             int32_t *targets, int32_t *peak_scores);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GB_CHAIN_H */

@@ -107,7 +107,53 @@ def fmi_golden():
     print("wrote fmi_golden.npz:", len(rid), "SMEMs for", len(lens), "reads")
 
 
+def chain_inputs(seed=41):
+    """Small call set exercising every branch of chain_dp: tiny calls, duplicate x (dr == 0),
+    multi-segment calls (n_segs > 1, seg ids in y bits 48..55), mixed strands, long calls."""
+    rng = np.random.default_rng(seed)
+    calls = gen.chain_dataset("small", num_calls=40, seed=seed, median_n=300, max_n=6000)
+    offs, xs, ys, aq, p4 = [0], [], [], [], []
+    for c in range(calls.ncalls):
+        o0, o1 = calls.offsets[c], calls.offsets[c + 1]
+        xs.append(calls.x[o0:o1]); ys.append(calls.y[o0:o1]); aq.append(calls.avg_qspan[c])
+        p4.append(calls.params4[c]); offs.append(offs[-1] + (o1 - o0))
+    extra = []
+    # n = 1 and n = 2
+    extra.append((np.array([5000], np.uint64), np.array([(15 << 32) | 100], np.uint64), 15.0, (5000, 5000, 500, 1)))
+    extra.append((np.array([5000, 5010], np.uint64), np.array([(15 << 32) | 100, (15 << 32) | 110], np.uint64), 15.0, (5000, 5000, 500, 1)))
+    # multi-segment (paired) call with duplicate positions and segment ids 0/1
+    n = 800
+    x = np.sort(rng.integers(10_000, 30_000, n)).astype(np.uint64)
+    x[100:110] = x[100]  # dr == 0 runs
+    seg = rng.integers(0, 2, n).astype(np.uint64)
+    q = rng.integers(0, 3000, n).astype(np.uint64)
+    y = (seg << np.uint64(48)) | (np.uint64(19) << np.uint64(32)) | q
+    extra.append((x, y, 19.0, (5000, 1000, 200, 2)))
+    # small max_dist / bw to hit those filters
+    x2, y2, a2 = gen.chain_call(rng, 3000)
+    extra.append((x2, y2, a2, (400, 300, 30, 1)))
+    for x, y, a, p in extra:
+        xs.append(np.asarray(x, np.uint64)); ys.append(np.asarray(y, np.uint64)); aq.append(a)
+        p4.append(np.array(p, np.int32)); offs.append(offs[-1] + len(x))
+    return gen.ChainCalls(np.array(offs), np.concatenate(xs), np.concatenate(ys), np.array(aq, np.float32),
+                          np.stack(p4))
+
+
+def chain_golden():
+    """chain_golden.npz: reference scalar chain_dp outputs (tools/minimap2-acceleration/kernel/scalar,
+    via oracle/_ref/libref_chain.so) for chain_inputs()."""
+    lib = oracle_lib.ref_chain()
+    if lib is None:
+        raise SystemExit("oracle/_ref/libref_chain.so missing: run `make -C oracle ref` first")
+    c = chain_inputs()
+    sc, par, tg, pk = oracle_lib.ref_chain_run(lib, c, 4)
+    np.savez_compressed(os.path.join(HERE, "chain_golden.npz"), offsets=c.offsets, x=c.x, y=c.y,
+                        avg_qspan=c.avg_qspan, params4=c.params4, scores=sc, parents=par, targets=tg, peaks=pk)
+    print("wrote chain_golden.npz:", c.ncalls, "calls,", c.nanchors, "anchors")
+
+
 def main():
+    chain_golden()
     fmi_golden()
     ref = oracle_lib.ref_phmm()
     if ref is None:

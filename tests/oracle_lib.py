@@ -44,3 +44,44 @@ def ref_phmm():
         lib.ref_phmm_has_avx512.restype = ctypes.c_int
         _ref = lib
     return _ref
+
+
+def _chain_decl(lib, fn):
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    getattr(lib, fn).argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+
+
+def chain_oracle(calls, nthreads=4):
+    """oracle/chain_oracle.c over a gen.ChainCalls -> (scores, parents, targets, peaks, visited)."""
+    import numpy as np
+    lib = oracle()
+    if not getattr(lib, "_chain_decl", False):
+        _chain_decl(lib, "chain_oracle_batch")
+        lib.chain_oracle_batch.restype = ctypes.c_int64
+        lib._chain_decl = True
+    n = calls.nanchors
+    out = [np.zeros(max(n, 1), np.int32) for _ in range(4)]
+    visited = lib.chain_oracle_batch(calls.ncalls, calls.offsets.ctypes.data, calls.avg_qspan.ctypes.data,
+                                     calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data,
+                                     *[o.ctypes.data for o in out], nthreads)
+    return [o[:n] for o in out] + [visited]
+
+
+def ref_chain():
+    path = os.path.join(ROOT, "oracle", "_ref", "libref_chain.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    _chain_decl(lib, "ref_chain_batch")
+    lib.ref_chain_batch.restype = None
+    return lib
+
+
+def ref_chain_run(lib, calls, nthreads=4):
+    import numpy as np
+    n = calls.nanchors
+    out = [np.zeros(max(n, 1), np.int32) for _ in range(4)]
+    lib.ref_chain_batch(calls.ncalls, calls.offsets.ctypes.data, calls.avg_qspan.ctypes.data,
+                        calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data,
+                        *[o.ctypes.data for o in out], nthreads)
+    return [o[:n] for o in out]

@@ -1,0 +1,72 @@
+"""chain_dp parity. CPU: the C restatement (oracle/chain_oracle.c) against the reference scalar kernel's
+golden outputs (tests/golden/chain_golden.npz) and, when built, the reference itself. GPU: the HIP
+kernel (csrc/chain.hip) against both, bit-exact on scores, parents, targets and peak scores."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from conftest import GOLDEN
+from genomicsbench_palisade_amd import gen
+
+
+@pytest.fixture(scope="module")
+def golden():
+    z = np.load(os.path.join(GOLDEN, "chain_golden.npz"))
+    calls = gen.ChainCalls(z["offsets"], z["x"], z["y"], z["avg_qspan"], z["params4"])
+    return calls, [z["scores"], z["parents"], z["targets"], z["peaks"]]
+
+
+NAMES = ["scores", "parents", "targets", "peak_scores"]
+
+
+def assert_same(got, exp):
+    for k, name in enumerate(NAMES):
+        bad = np.nonzero(got[k] != exp[k])[0]
+        assert len(bad) == 0, f"{name}: {len(bad)} mismatches, first at {bad[:5]}: {got[k][bad[:5]]} vs {exp[k][bad[:5]]}"
+
+
+def test_oracle_vs_golden(golden):
+    calls, exp = golden
+    got = oracle_lib.chain_oracle(calls)
+    assert_same(got, exp)
+    assert got[4] > calls.nanchors  # visited pairs
+
+
+def test_oracle_vs_reference_live():
+    lib = oracle_lib.ref_chain()
+    if lib is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    calls = gen.chain_dataset("small", num_calls=120, seed=77, median_n=800, max_n=30000)
+    assert_same(oracle_lib.chain_oracle(calls), oracle_lib.ref_chain_run(lib, calls))
+
+
+@pytest.mark.gpu
+def test_gpu_vs_golden(golden):
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    calls, exp = golden
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == oracle_lib.chain_oracle(calls)[4]
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,ncalls,median,maxn", [(1, 300, 1500, 87271), (2, 2000, 200, 5000)])
+def test_gpu_vs_oracle(seed, ncalls, median, maxn):
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    calls = gen.chain_dataset("small", num_calls=ncalls, seed=seed, median_n=median, max_n=maxn)
+    exp = oracle_lib.chain_oracle(calls, 8)
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
+    b.run()
+    assert_same(b.results(), exp)  # re-run on the same device buffers
+    b.close()
