@@ -7,6 +7,9 @@ Metric (BASELINE.json): "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8
 phmm (the line's `value`): a step = one PairHMM forward pass (f32 kernel + f64 fallback kernel +
 log10 epilogue) over one 'large'-shaped synthetic job of B batches (gen.phmm_dataset, seed 1 + rank)
 already resident in HBM; value = total cells of all ranks x K / max-over-ranks wall time, in GCUPS.
+chain / bsw (the "chain" / "bsw" objects): a step = chain_dp over every call of a 'large'-shaped
+set (10k calls, 25 M anchors, seed 5 + rank; Manchors/s) / the banded SW extension of every pair of
+a 'large'-shaped set (10 606 460 pairs, seed 11 + rank; GCUPS over the reference's inner-loop cells).
 fmi (the line's "fmi" object): a step = the whole fmi.cpp per-batch pipeline (SMEMs, reseeding,
 LAST seeds, per-read sort) over every read of the rank's shard (gen.fmi_reads, seed 8 + rank) against
 a 512 Mbp genome-like synthetic reference (+RC: 1.024 G BWT rows, 1.02 GB CP_OCC) built on the GPU;
@@ -34,6 +37,10 @@ PEAK_F64_OPS = PEAK_F32_OPS / 2      # FP64 vector peak 78.6 TF (FMA=2) -> 39.3e
 PHMM_FLOP_PER_CELL = 12              # 12 FP ops per cell, no FMA
 PEAK_HBM = 8.0e12                    # HBM3E spec bytes/s (MI355X_MICROARCH.md)
 FMI_BYTES_PER_EXT = 128              # 2 x 64-B CP_OCC lines per backwardExt
+CHAIN_OPS_PER_PAIR = 25              # ~25 int32/fp64 ops per visited (i, j) pair
+PEAK_CHAIN_OPS = PEAK_F64_OPS        # INT32/FP64 VALU, 39.3e12 lane-op/s
+BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar inner-loop iteration
+PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
 def log(msg):
@@ -160,6 +167,173 @@ def cpu_baseline_fmi(oracle_index, codes, lens, sample_seconds: float):
                       f"FMI_search (batches of 512 over {threads} threads), {t:.1f} s"}
 
 
+def _cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline_chain(calls, sample_seconds: float):
+    """The reference's scalar chain_dp (tools/minimap2-acceleration/kernel/scalar, compiled from the
+    reference tree into oracle/_ref, kind 'reference'; the C restatement when absent, kind 'port')
+    over a bounded random sample of the same calls, OpenMP over calls like host_chain_kernel."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    from genomicsbench_palisade_amd import gen
+    threads = max(1, min(16, _cores()))
+    ref = oracle_lib.ref_chain()
+    rng = np.random.default_rng(321)
+    order = rng.permutation(calls.ncalls)
+
+    def sub(idx):
+        idx = np.sort(idx)
+        lens = calls.offsets[idx + 1] - calls.offsets[idx]
+        offs = np.zeros(len(idx) + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        sel = np.concatenate([np.arange(calls.offsets[c], calls.offsets[c + 1]) for c in idx])
+        return gen.ChainCalls(offs, calls.x[sel], calls.y[sel], calls.avg_qspan[idx], calls.params4[idx])
+
+    def run(c):
+        t0 = time.perf_counter()
+        if ref is not None:
+            oracle_lib.ref_chain_run(ref, c, threads)
+        else:
+            oracle_lib.chain_oracle(c, threads)
+        return time.perf_counter() - t0
+
+    cal = sub(order[:64])
+    rate = cal.nanchors / max(run(cal), 1e-6)
+    cum = np.cumsum((calls.offsets[order + 1] - calls.offsets[order]))
+    m = int(min(calls.ncalls, max(64, np.searchsorted(cum, rate * sample_seconds))))
+    s_ = sub(order[:m])
+    t = run(s_)
+    return {"value": s_.nanchors / t / 1e6, "unit": "Manchors/s", "cores": threads,
+            "kind": "reference" if ref is not None else "port",
+            "sample": f"{m} of {calls.ncalls} calls ({s_.nanchors} anchors, random) of the same set, "
+                      f"{'minimap2-acceleration scalar chain_dp' if ref is not None else 'C restatement'}, "
+                      f"OpenMP {threads} threads, {t:.1f} s"}
+
+
+def cpu_baseline_bsw(pairs, params, sample_seconds: float):
+    """bwa v1 ksw_extend2 compiled from the reference tree (oracle/_ref/libref_bwa.so) -- the function
+    the benchmark's scalarBandedSWA (bandedSWA.cpp:130-251) restates; the benchmark's own SSE
+    getScores16 needs Palisade and is not buildable here -- on a bounded random sample of the same
+    pairs, one pair stream per thread (ctypes releases the GIL). Falls back to the C restatement."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    from concurrent.futures import ThreadPoolExecutor
+    threads = max(1, min(16, _cores()))
+    ref = oracle_lib.ref_bsw()
+    rng = np.random.default_rng(654)
+
+    def run(sub):
+        parts = [sub.subset(np.arange(k, sub.n, threads)) for k in range(threads)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            if ref is not None:
+                list(ex.map(lambda q: oracle_lib.ref_bsw_run(ref, q, params), parts))
+            else:
+                list(ex.map(lambda q: oracle_lib.bsw_oracle(q, params, 1), parts))
+        return time.perf_counter() - t0
+
+    cal = pairs.subset(rng.choice(pairs.n, 4000 * threads, replace=False))
+    rate = cal.n / max(run(cal), 1e-6)
+    m = int(min(pairs.n, max(cal.n, rate * sample_seconds)))
+    idx = np.sort(rng.choice(pairs.n, m, replace=False))
+    sub = pairs.subset(idx)
+    cells = oracle_lib.bsw_oracle(sub, params, threads)[2]
+    t = run(sub)
+    return {"value": cells / t / 1e9, "unit": "GCUPS", "cores": threads,
+            "kind": "reference" if ref is not None else "port", "pairs_per_s": m / t,
+            "sample": f"{m} of {pairs.n} pairs (random) of the same set, "
+                      f"{'bwa ksw_extend2 (tools/bwa/ksw.c)' if ref is not None else 'C restatement'}, "
+                      f"{threads} threads, {t:.1f} s"}
+
+
+def bench_chain(args, D, rank, world):
+    from genomicsbench_palisade_amd import chain, gen
+    log("chain: generating calls")
+    calls = gen.chain_dataset("large", seed=5 + rank)
+    b = chain.ChainBatch(calls)
+    for _ in range(args.warmup):
+        b.run()
+        b.sync()
+    visited = b.results()[4]
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    ks = []
+    for _ in range(args.steps):
+        b.run()
+        b.sync()
+        ks.append(b.timing())
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    manch = D.sum(float(calls.nanchors)) * args.steps / elapsed / 1e6
+    ms = float(np.mean(ks))
+    ach = CHAIN_OPS_PER_PAIR * visited / (ms * 1e-3)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("chain: CPU baseline")
+        cpu = cpu_baseline_chain(calls, args.cpu_seconds)
+    b.close()
+    return {
+        "value": round(manch, 3), "unit": "Manchors/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": f"chain large: {calls.ncalls} calls, {calls.nanchors} anchors/rank (lognormal "
+                               f"n, median 1500, max 87271), max_dist 5000, bw 500, n_segs 1",
+                   "visited_pairs": int(visited), "gpairs_per_s": visited * args.steps * D.world / elapsed / 1e9},
+        "roofline": {"bound": "valu", "kernel": "chain_kernel", "achieved": ach / 1e12, "peak": PEAK_CHAIN_OPS / 1e12,
+                     "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": None,
+                     "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
+        "kernels_ms": {"chain_kernel": ms},
+        "cpu_baseline": cpu,
+    }
+
+
+def bench_bsw(args, D, rank, world):
+    from genomicsbench_palisade_amd import bsw, gen
+    log("bsw: generating pairs")
+    pairs = gen.bsw_dataset(args.bsw_pairs, seed=11 + rank, threads=min(16, _cores()))
+    params = bsw.default_params()
+    b = bsw.BswBatch(pairs, params)
+    for _ in range(args.warmup):
+        b.run()
+        b.sync()
+    _, _, cells = b.results(want_cells=False)
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    ks = []
+    for _ in range(args.steps):
+        b.run()
+        b.sync()
+        ks.append(b.timing())
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    gcups = D.sum(float(cells)) * args.steps / elapsed / 1e9
+    ms = float(np.mean(ks))
+    ach = BSW_OPS_PER_CELL * cells / (ms * 1e-3)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("bsw: CPU baseline")
+        cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds)
+    b.close()
+    return {
+        "value": round(gcups, 3), "unit": "GCUPS", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": f"bsw large: {pairs.n} pairs/rank, query U[10,150], target = mutated query + "
+                               f"U[0,100], h0 0 (20%) or U[10,70], w 100, zdrop 100",
+                   "cells": int(cells), "mpairs_per_s": pairs.n * D.world * args.steps / elapsed / 1e6},
+        "roofline": {"bound": "valu", "kernel": "bsw_extend_kernel", "achieved": ach / 1e12,
+                     "peak": PEAK_INT_OPS / 1e12, "unit": "T int op/s", "frac": ach / PEAK_INT_OPS,
+                     "traffic": None, "ops_per_cell": BSW_OPS_PER_CELL},
+        "kernels_ms": {"bsw_extend_kernel": ms},
+        "cpu_baseline": cpu,
+    }
+
+
 def bench_phmm(args, D, rank, world):
     import genomicsbench_palisade_amd as gb  # noqa: F401
     from genomicsbench_palisade_amd import gen, phmm
@@ -280,7 +454,8 @@ def main():
     ap.add_argument("--batches", type=int, default=16, help="'large' phmm batches per job (per rank)")
     ap.add_argument("--fmi-reads", type=int, default=10_000_000, help="fmi reads per rank")
     ap.add_argument("--fmi-ref-mbp", type=float, default=512.0)
-    ap.add_argument("--only", choices=["phmm", "fmi"], default=None)
+    ap.add_argument("--bsw-pairs", type=int, default=10_606_460, help="bsw pairs per rank (large set)")
+    ap.add_argument("--only", default=None, help="comma list of legs: phmm,fmi,chain,bsw (default all)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -290,8 +465,11 @@ def main():
     import genomicsbench_palisade_amd as gb
     gb.set_device(local)
 
-    ph = bench_phmm(args, D, rank, world) if args.only != "fmi" else None
-    fm = bench_fmi(args, D, rank, world) if args.only != "phmm" else None
+    legs = set((args.only or "phmm,fmi,chain,bsw").split(","))
+    ph = bench_phmm(args, D, rank, world) if "phmm" in legs else None
+    fm = bench_fmi(args, D, rank, world) if "fmi" in legs else None
+    ch = bench_chain(args, D, rank, world) if "chain" in legs else None
+    bw = bench_bsw(args, D, rank, world) if "bsw" in legs else None
 
     if rank == 0:
         line = {
@@ -305,9 +483,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32+f64 (phmm), int64 (fmi)",
+            "dtype": "f32+f64 (phmm), int64 (fmi), int32/f64 (chain), int32 (bsw)",
             "data": "synthetic ('large'-shaped PairHMM batches seed 1+rank; genome-like reference seed 7 "
-                    "+ 151 bp reads seed 8+rank for fmi)",
+                    "+ 151 bp reads seed 8+rank for fmi; minimap2-shaped anchor calls seed 5+rank for chain; "
+                    "extension pairs seed 11+rank for bsw)",
             "config": {"workload": ("phmm large: %d batches/rank, %d testcases, %.3f G cells/rank/step, "
                                     "%.1f%% testcases on the f64 fallback" % (
                                         args.batches, ph["ntc"], ph["cells"] / 1e9, 100 * ph["f64_frac"]))
@@ -317,6 +496,8 @@ def main():
             "kernels_ms": ph["kernels_ms"] if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
             "fmi": fm,
+            "chain": ch,
+            "bsw": bw,
         }
         print(json.dumps(line))
     D.close()

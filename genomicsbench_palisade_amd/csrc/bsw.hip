@@ -1,0 +1,453 @@
+// bsw.hip -- MI355X (gfx950) banded Smith-Waterman extension (GenomicsBench bsw): kernel and C ABI.
+//
+// Semantics: benchmarks/bsw/bandedSWA.cpp:130-251 (scalarBandedSWA == bwa ksw_extend2), which the
+// benchmark's 16-bit SIMD getScores16 reproduces. Integer arithmetic
+// throughout, so results are bit-exact by construction.
+//
+// MI355X design: one pair per wave64, lanes across the query, lane l owning the K = ceil((qlen+1)/64)
+// consecutive DP columns j = l*K .. l*K+K-1 (the eh[] entries 0..qlen of the reference live in
+// registers for the whole pair, so stale entries outside the band persist exactly as in the
+// reference's array). Rows (target bases) are processed in order; within a row the only sequential
+// dependency is F, and F(i, j) = max(0, max_{beg<=k<j} (max(M_k - oe_ins, 0) - e_ins (j-1-k)))
+// depends on the previous row only (M_k = H(i-1,k-1) + S), so a row is one max-plus prefix scan:
+// in-lane over the K columns, then across lanes with DPP (row_shr 1/2/4/8, row_bcast 15/31).
+// Row control (band, row max / last argmax, gscore, zdrop, band narrowing) is wave-uniform scalar
+// code fed by one DPP max-reduction and three ballots per row. Waves pull pairs from an atomic
+// counter (persistent grid), so ragged pairs balance across the 256 CUs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gb_bsw.h"
+#include "gb_common.h"
+
+static_assert(sizeof(gb_seqpair) == 72, "gb_seqpair must match SeqPair (bandedSWA.h:92-101)");
+
+namespace gbbsw {
+
+constexpr int kNeg = -(1 << 28);
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlocksPerCU = 8;
+
+struct Pair {  // device descriptor, 32 B
+  int64_t t_off, q_off;
+  int32_t tlen, qlen, h0, w;  // w: band after the max_ins / max_del adjustment (bandedSWA.cpp:161-170)
+};
+
+struct Args {
+  const Pair *pairs;
+  int64_t n;
+  const uint8_t *tgt, *qry;
+  int32_t *out6, *cells;
+  unsigned long long *total_cells;
+  unsigned int *next;
+  int o_del, e_del, o_ins, e_ins, zdrop;
+  int8_t mat[28];
+};
+
+// wave-wide inclusive max scan (Hillis-Steele in 16-lane rows, then row broadcasts)
+__device__ __forceinline__ int scan_max(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(kNeg, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ int shr1(int v, int lane0) {
+  return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+template <int K>
+__device__ __forceinline__ void extend(const Args &A, const Pair &P, const int8_t *smat, int lane,
+                                       int32_t *o6, int &ncells) {
+  const int qlen = P.qlen, tlen = P.tlen, h0 = P.h0, w = P.w;
+  const int o_del = A.o_del, e_del = A.e_del, o_ins = A.o_ins, e_ins = A.e_ins;
+  const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+  const uint8_t *qry = A.qry + P.q_off;
+  const uint8_t *tgt = A.tgt + P.t_off;
+
+  int H[K], E[K], plo[K], phi[K], ej[K];
+  const int v1 = max(h0 - oe_ins, 0);
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const int j = lane * K + c;
+    int qb = 4;
+    if (j < qlen) qb = min((int)qry[j], 4);
+    plo[c] = (smat[qb] & 0xFF) | (smat[5 + qb] & 0xFF) << 8 | (smat[10 + qb] & 0xFF) << 16 |
+             (smat[15 + qb] & 0xFF) << 24;
+    phi[c] = smat[20 + qb];
+    // first row (bandedSWA.cpp:157-159): h0, then h0 - oe_ins decreasing by e_ins down to 0
+    H[c] = j == 0 ? h0 : (j <= qlen ? max(v1 - (j - 1) * e_ins, 0) : 0);
+    E[c] = 0;
+    ej[c] = e_ins * j;
+  }
+
+  int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+  int tword = 0;
+  int i;
+  for (i = 0; i < tlen; ++i) {
+    const int ir = i & 255;
+    if (ir == 0) {  // 256 target bases per VGPR: lane l holds bases i+4l .. i+4l+3
+      tword = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int t = i + 4 * lane + b;
+        if (t < tlen) tword |= (int)tgt[t] << (8 * b);
+      }
+    }
+    const int tb = min((__builtin_amdgcn_readlane(tword, ir >> 2) >> (8 * (ir & 3))) & 0xFF, 4);
+    const int sh = 8 * (tb & 3);
+    const bool hi = tb >= 4;
+    // band (bandedSWA.cpp:180-182)
+    if (beg < i - w) beg = i - w;
+    if (end > i + w + 1) end = i + w + 1;
+    if (end > qlen) end = qlen;
+    const int h1init = beg == 0 ? max(h0 - (o_del + e_del * (i + 1)), 0) : 0;
+    ncells += max(end - beg, 0);
+
+    int M[K], g[K], lpx[K], h[K], En[K];
+    bool inb[K];
+    int lp = kNeg;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const int j = lane * K + c;
+      inb[c] = j >= beg && j < end;
+      const int s = __builtin_amdgcn_sbfe(hi ? phi[c] : plo[c], sh, 8);
+      const int Mv = H[c] ? H[c] + s : 0;  // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0
+      M[c] = Mv;
+      g[c] = inb[c] ? max(Mv - oe_ins, 0) + ej[c] : kNeg;
+      lpx[c] = lp;
+      lp = max(lp, g[c]);
+    }
+    const int lex = shr1(scan_max(lp), kNeg);
+    int hm = -1;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const int f = max(max(lex, lpx[c]) - ej[c] + e_ins, 0);  // F(i,j)
+      h[c] = max(max(M[c], E[c]), f);
+      En[c] = max(max(E[c] - e_del, M[c] - oe_del), 0);  // E(i+1,j)
+      if (inb[c]) hm = max(hm, h[c]);
+    }
+    const int m = max(__builtin_amdgcn_readlane(scan_max(hm), 63), 0);
+    int mj = -1;
+    if (m > 0) {  // last column reaching the row maximum (bandedSWA.cpp:203-204)
+      int jl = -1;
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+        if (inb[c] && h[c] == m) jl = lane * K + c;
+      const uint64_t bal = ballot(jl >= 0);
+      mj = __builtin_amdgcn_readlane(jl, 63 - __builtin_clzll(bal));
+    }
+    // eh[j].h <- H(i,j-1) for j in (beg, end], eh[beg].h <- first column, eh[j].e <- E(i+1,j),
+    // eh[end].e <- 0 (bandedSWA.cpp:195-197,217)
+    const int wlo = min(beg, end);
+    const int hprev = shr1(h[K - 1], 0);
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const int j = lane * K + c;
+      const int hs = c ? h[c - 1] : hprev;
+      if (j >= wlo && j <= end) {
+        H[c] = j == wlo ? h1init : hs;
+        E[c] = j == end ? 0 : En[c];
+      }
+    }
+    const int ce = end % K;
+    int hsel = H[0];
+#pragma unroll
+    for (int c = 1; c < K; ++c)
+      if (ce == c) hsel = H[c];
+    const int h1 = __builtin_amdgcn_readlane(hsel, end / K);
+    if ((beg < end ? end : beg) == qlen) {  // bandedSWA.cpp:218-221
+      max_ie = gscore > h1 ? max_ie : i;
+      gscore = gscore > h1 ? gscore : h1;
+    }
+    if (m == 0) break;
+    if (m > mx) {
+      mx = m, max_i = i, max_j = mj;
+      max_off = max(max_off, abs(mj - i));
+    } else if (A.zdrop > 0) {
+      if (i - max_i > mj - max_j) {
+        if (mx - m - ((i - max_i) - (mj - max_j)) * e_del > A.zdrop) break;
+      } else {
+        if (mx - m - ((mj - max_j) - (i - max_i)) * e_ins > A.zdrop) break;
+      }
+    }
+    // band narrowing (bandedSWA.cpp:235-239)
+    int jf = INT_MAX;
+#pragma unroll
+    for (int c = K - 1; c >= 0; --c) {
+      const int j = lane * K + c;
+      if ((H[c] | E[c]) != 0 && j >= beg && j < end) jf = j;
+    }
+    const uint64_t bf = ballot(jf != INT_MAX);
+    const int nb = bf ? __builtin_amdgcn_readlane(jf, __builtin_ctzll(bf)) : end;
+    int jl = -1;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const int j = lane * K + c;
+      if ((H[c] | E[c]) != 0 && j >= nb && j <= end) jl = j;
+    }
+    const uint64_t bl = ballot(jl >= 0);
+    const int je = bl ? __builtin_amdgcn_readlane(jl, 63 - __builtin_clzll(bl)) : nb - 1;
+    beg = nb;
+    end = je + 2 < qlen ? je + 2 : qlen;
+  }
+  if (lane == 0) {
+    o6[0] = mx;
+    o6[1] = max_j + 1;
+    o6[2] = max_i + 1;
+    o6[3] = max_ie + 1;
+    o6[4] = gscore;
+    o6[5] = max_off;
+  }
+}
+
+__global__ __launch_bounds__(64 * kWavesPerBlock) void bsw_extend_kernel(Args A) {
+  __shared__ int8_t smat[32];
+  if (threadIdx.x < 25) smat[threadIdx.x] = A.mat[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  unsigned long long wave_cells = 0;
+  for (;;) {
+    unsigned int p = 0;
+    if (lane == 0) p = atomicAdd(A.next, 1u);
+    p = __builtin_amdgcn_readfirstlane(p);
+    if ((int64_t)p >= A.n) break;
+    const Pair P = A.pairs[p];
+    int nc = 0;
+    int32_t *o6 = A.out6 + 6 * (int64_t)p;
+    const int K = (P.qlen + 64) >> 6;  // columns 0..qlen
+    if (K <= 1)
+      extend<1>(A, P, smat, lane, o6, nc);
+    else if (K == 2)
+      extend<2>(A, P, smat, lane, o6, nc);
+    else if (K == 3)
+      extend<3>(A, P, smat, lane, o6, nc);
+    else
+      extend<4>(A, P, smat, lane, o6, nc);
+    if (lane == 0) A.cells[p] = nc;
+    wave_cells += (unsigned)nc;
+  }
+  if (lane == 0 && wave_cells) atomicAdd(A.total_cells, wave_cells);
+}
+
+// band adjustment of bandedSWA.cpp:161-170, in the reference's double arithmetic
+static int adjust_w(int w, int qlen, int mx, const gb_bsw_params &p) {
+  int max_ins = (int)((double)(qlen * mx + p.end_bonus - p.o_ins) / p.e_ins + 1.);
+  max_ins = max_ins > 1 ? max_ins : 1;
+  w = w < max_ins ? w : max_ins;
+  int max_del = (int)((double)(qlen * mx + p.end_bonus - p.o_del) / p.e_del + 1.);
+  max_del = max_del > 1 ? max_del : 1;
+  return w < max_del ? w : max_del;
+}
+
+}  // namespace gbbsw
+
+struct gb_bsw_batch {
+  int device = -1, num_cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  gb_bsw_params params{};
+  int64_t n = 0;
+  gbbsw::Pair *d_pairs = nullptr;
+  uint8_t *d_tgt = nullptr, *d_qry = nullptr;
+  int32_t *d_out6 = nullptr, *d_cells = nullptr;
+  unsigned long long *d_total = nullptr;  // [0] total cells, [1] work counter
+  bool ran = false;
+};
+
+extern "C" {
+
+void gb_bsw_fill_scmat(int a, int b, int ambig, int8_t mat[25]) {
+  int k = 0;
+  for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) mat[k++] = (int8_t)(i == j ? a : -b);
+    mat[k++] = (int8_t)ambig;
+  }
+  for (int j = 0; j < 5; ++j) mat[k++] = (int8_t)ambig;
+}
+
+void gb_bsw_default_params(gb_bsw_params *p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->o_del = p->o_ins = 6;
+  p->e_del = p->e_ins = 1;
+  p->zdrop = 100;
+  p->end_bonus = 5;
+  p->w = 100;
+  gb_bsw_fill_scmat(1, 4, -1, p->mat);
+}
+
+int gb_bsw_batch_destroy(gb_bsw_batch *B) {
+  if (!B) return GB_OK;
+  if (B->device >= 0) hipSetDevice(B->device);
+  if (B->stream) hipStreamSynchronize(B->stream);
+  hipFree(B->d_pairs);
+  hipFree(B->d_tgt);
+  hipFree(B->d_qry);
+  hipFree(B->d_out6);
+  hipFree(B->d_cells);
+  hipFree(B->d_total);
+  for (auto &e : B->ev)
+    if (e) hipEventDestroy(e);
+  if (B->stream) hipStreamDestroy(B->stream);
+  delete B;
+  return GB_OK;
+}
+
+int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, int64_t n,
+                        const uint8_t *ref, int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes,
+                        gb_bsw_batch **out) {
+  GB_ARG(out && params && n >= 0 && (n == 0 || pairs), "gb_bsw_batch_create: bad arguments");
+  *out = nullptr;
+  GB_ARG(n < (1ll << 32) - 1, "gb_bsw_batch_create: too many pairs");
+  GB_ARG(params->e_del > 0 && params->e_ins > 0, "gb_bsw_batch_create: gap extension must be > 0");
+  GB_ARG(ref_bytes >= 0 && qer_bytes >= 0 && (ref_bytes == 0 || ref) && (qer_bytes == 0 || qer),
+         "gb_bsw_batch_create: bad sequence buffers");
+  int mx = 0;
+  for (int k = 0; k < 25; ++k) mx = std::max(mx, (int)params->mat[k]);
+  std::vector<gbbsw::Pair> P((size_t)n);
+  for (int64_t p = 0; p < n; ++p) {
+    const gb_seqpair &s = pairs[p];
+    GB_ARG(s.len2 >= 1 && s.len2 <= GB_BSW_MAX_QLEN && s.len1 >= 0,
+           "gb_bsw_batch_create: pair %lld has len1=%d len2=%d (need len2 in [1,%d])", (long long)p,
+           s.len1, s.len2, GB_BSW_MAX_QLEN);
+    GB_ARG(s.idr >= 0 && s.idr + s.len1 <= ref_bytes && s.idq >= 0 && s.idq + s.len2 <= qer_bytes,
+           "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
+    P[p] = {s.idr, s.idq, s.len1, s.len2, s.h0, gbbsw::adjust_w(params->w, s.len2, mx, *params)};
+  }
+  auto *B = new gb_bsw_batch();
+  B->params = *params;
+  B->n = n;
+  hipError_t e = hipGetDevice(&B->device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&B->num_cus, hipDeviceAttributeMultiprocessorCount, B->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
+  for (auto &ev : B->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  if (e == hipSuccess) e = hipMalloc(&B->d_pairs, nn * sizeof(gbbsw::Pair));
+  if (e == hipSuccess) e = hipMalloc(&B->d_tgt, (size_t)std::max<int64_t>(ref_bytes, 1));
+  if (e == hipSuccess) e = hipMalloc(&B->d_qry, (size_t)std::max<int64_t>(qer_bytes, 1));
+  if (e == hipSuccess) e = hipMalloc(&B->d_out6, nn * 6 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_cells, nn * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&B->d_total, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess && n) e = hipMemcpy(B->d_pairs, P.data(), (size_t)n * sizeof(gbbsw::Pair), hipMemcpyHostToDevice);
+  if (e == hipSuccess && ref_bytes) e = hipMemcpy(B->d_tgt, ref, (size_t)ref_bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess && qer_bytes) e = hipMemcpy(B->d_qry, qer, (size_t)qer_bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    gb::set_error("gb_bsw_batch_create: %s", hipGetErrorString(e));
+    gb_bsw_batch_destroy(B);
+    return GB_ERR_HIP;
+  }
+  *out = B;
+  return GB_OK;
+}
+
+int gb_bsw_batch_run(gb_bsw_batch *B) {
+  GB_ARG(B, "gb_bsw_batch_run: null batch");
+  GB_HIP(hipSetDevice(B->device));
+  GB_HIP(hipMemsetAsync(B->d_total, 0, 2 * sizeof(unsigned long long), B->stream));
+  GB_HIP(hipEventRecord(B->ev[0], B->stream));
+  if (B->n > 0) {
+    gbbsw::Args A;
+    A.pairs = B->d_pairs;
+    A.n = B->n;
+    A.tgt = B->d_tgt;
+    A.qry = B->d_qry;
+    A.out6 = B->d_out6;
+    A.cells = B->d_cells;
+    A.total_cells = B->d_total;
+    A.next = reinterpret_cast<unsigned int *>(B->d_total + 1);
+    A.o_del = B->params.o_del;
+    A.e_del = B->params.e_del;
+    A.o_ins = B->params.o_ins;
+    A.e_ins = B->params.e_ins;
+    A.zdrop = B->params.zdrop;
+    std::memset(A.mat, 0, sizeof(A.mat));
+    std::memcpy(A.mat, B->params.mat, 25);
+    const int64_t waves = B->n;
+    const int64_t cap = (int64_t)B->num_cus * gbbsw::kBlocksPerCU;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cap, (waves + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
+    hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0,
+                       B->stream, A);
+    GB_HIP(hipGetLastError());
+  }
+  GB_HIP(hipEventRecord(B->ev[1], B->stream));
+  B->ran = true;
+  return GB_OK;
+}
+
+int gb_bsw_batch_sync(gb_bsw_batch *B) {
+  GB_ARG(B, "gb_bsw_batch_sync: null batch");
+  GB_HIP(hipStreamSynchronize(B->stream));
+  return GB_OK;
+}
+
+int gb_bsw_batch_results(gb_bsw_batch *B, gb_seqpair *pairs, int32_t *out6, int32_t *cells,
+                         int64_t *total_cells) {
+  GB_ARG(B, "gb_bsw_batch_results: null batch");
+  if (!B->ran) {
+    gb::set_error("gb_bsw_batch_results: batch has not been run");
+    return GB_ERR_STATE;
+  }
+  GB_HIP(hipSetDevice(B->device));
+  GB_HIP(hipStreamSynchronize(B->stream));
+  const size_t n = (size_t)B->n;
+  std::vector<int32_t> o;
+  if (n && (pairs || out6)) {
+    int32_t *dst = out6;
+    if (!dst) {
+      o.resize(6 * n);
+      dst = o.data();
+    }
+    GB_HIP(hipMemcpy(dst, B->d_out6, n * 6 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (pairs)
+      for (size_t p = 0; p < n; ++p) {
+        const int32_t *r = dst + 6 * p;
+        pairs[p].score = r[0];
+        pairs[p].qle = r[1];
+        pairs[p].tle = r[2];
+        pairs[p].gtle = r[3];
+        pairs[p].gscore = r[4];
+        pairs[p].max_off = r[5];
+      }
+  }
+  if (n && cells) GB_HIP(hipMemcpy(cells, B->d_cells, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (total_cells) {
+    unsigned long long t = 0;
+    GB_HIP(hipMemcpy(&t, B->d_total, sizeof(t), hipMemcpyDeviceToHost));
+    *total_cells = (int64_t)t;
+  }
+  return GB_OK;
+}
+
+int gb_bsw_batch_timing(gb_bsw_batch *B, float *kernel_ms) {
+  GB_ARG(B && kernel_ms, "gb_bsw_batch_timing: bad arguments");
+  if (!B->ran) {
+    gb::set_error("gb_bsw_batch_timing: batch has not been run");
+    return GB_ERR_STATE;
+  }
+  GB_HIP(hipEventSynchronize(B->ev[1]));
+  GB_HIP(hipEventElapsedTime(kernel_ms, B->ev[0], B->ev[1]));
+  return GB_OK;
+}
+
+int gb_bsw_get_scores16(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
+                        int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes) {
+  gb_bsw_batch *B = nullptr;
+  int st = gb_bsw_batch_create(params, pairs, n, ref, ref_bytes, qer, qer_bytes, &B);
+  if (st) return st;
+  st = gb_bsw_batch_run(B);
+  if (!st) st = gb_bsw_batch_results(B, pairs, nullptr, nullptr, nullptr);
+  gb_bsw_batch_destroy(B);
+  return st;
+}
+
+}  // extern "C"

@@ -281,3 +281,101 @@ def write_chain_file(path, calls: ChainCalls):
             for xx, yy in zip(calls.x[o0:o1].tolist(), calls.y[o0:o1].tolist()):
                 f.write(f"{xx}\t{yy}\n")
             f.write("EOR\n")
+
+
+class BswPairs:
+    """Flattened bsw pairs: pair p has target (ref) tgt[toff[p]:toff[p]+tlen[p]] and query
+    qry[qoff[p]:qoff[p]+qlen[p]], codes 0..4 (loadPairs subtracts '0', main_banded.cpp:190-195)."""
+
+    def __init__(self, tgt, toff, tlen, qry, qoff, qlen, h0):
+        self.tgt, self.toff, self.tlen = tgt, toff, tlen
+        self.qry, self.qoff, self.qlen = qry, qoff, qlen
+        self.h0 = h0
+
+    @property
+    def n(self):
+        return len(self.h0)
+
+    def subset(self, idx):
+        idx = np.asarray(idx, np.int64)
+        tl, ql = self.tlen[idx], self.qlen[idx]
+        toff = np.zeros(len(idx), np.int64)
+        qoff = np.zeros(len(idx), np.int64)
+        toff[1:] = np.cumsum(tl)[:-1]
+        qoff[1:] = np.cumsum(ql)[:-1]
+        tgt = np.concatenate([self.tgt[self.toff[p]:self.toff[p] + self.tlen[p]] for p in idx.tolist()]) \
+            if len(idx) else np.zeros(0, np.uint8)
+        qry = np.concatenate([self.qry[self.qoff[p]:self.qoff[p] + self.qlen[p]] for p in idx.tolist()]) \
+            if len(idx) else np.zeros(0, np.uint8)
+        return BswPairs(tgt, toff, tl.copy(), qry, qoff, ql.copy(), self.h0[idx].copy())
+
+
+def _ragged_local(lens):
+    """(pair index, position within pair) for every element of a ragged concatenation."""
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens)[:-1]
+    tot = int(np.sum(lens))
+    pid = np.repeat(np.arange(len(lens), dtype=np.int64), lens)
+    return offs, pid, np.arange(tot, dtype=np.int64) - offs[pid]
+
+
+def bsw_pairs(num_pairs: int, seed: int = 11, qlen=(10, 150), extra=(0, 100), n_rate=0.002):
+    """bwa-mem-like extension pairs: query ~ U[10,150], target = query
+    mutated (per-pair substitution rate 0-12 %, one indel of +-1..6 bp in 30 % of pairs, 8 % of
+    targets unrelated) followed by U[0,100] extra bases; h0 = 0 for 20 %, else U[10,70]."""
+    rng = np.random.default_rng(seed)
+    n = int(num_pairs)
+    ql = rng.integers(qlen[0], qlen[1] + 1, n).astype(np.int32)
+    tl = (ql + rng.integers(extra[0], extra[1] + 1, n)).astype(np.int32)
+    h0 = np.where(rng.random(n) < 0.2, 0, rng.integers(10, 71, n)).astype(np.int32)
+    qoff, qpid, _ = _ragged_local(ql)
+    qry = rng.integers(0, 4, int(ql.sum())).astype(np.uint8)
+    qry[rng.random(len(qry)) < n_rate] = 4
+    toff, tpid, k = _ragged_local(tl)
+    brk = (rng.random(n) * ql).astype(np.int64)
+    dlt = rng.integers(1, 7, n) * np.where(rng.random(n) < 0.5, -1, 1)
+    dlt[rng.random(n) >= 0.3] = 0
+    src = k + np.where(k >= brk[tpid], dlt[tpid], 0)
+    ok = (src >= 0) & (src < ql[tpid]) & (rng.random(n) >= 0.08)[tpid]
+    tgt = rng.integers(0, 4, len(k)).astype(np.uint8)
+    tgt[ok] = qry[qoff[tpid[ok]] + src[ok]]
+    sub = rng.random(n) * 0.12
+    m = rng.random(len(tgt)) < sub[tpid]
+    tgt[m] = rng.integers(0, 4, int(m.sum())).astype(np.uint8)
+    tgt[rng.random(len(tgt)) < n_rate] = 4
+    return BswPairs(tgt, toff, tl, qry, qoff, ql, h0)
+
+
+def write_bsw_file(path, pairs: BswPairs):
+    """loadPairs format (main_banded.cpp:160-202): per pair 'h0', target, query lines of '0'..'4'."""
+    with open(path, "wb") as f:
+        for p in range(pairs.n):
+            t = (pairs.tgt[pairs.toff[p]:pairs.toff[p] + pairs.tlen[p]] + 48).tobytes()
+            q = (pairs.qry[pairs.qoff[p]:pairs.qoff[p] + pairs.qlen[p]] + 48).tobytes()
+            f.write(b"%d\n%s\n%s\n" % (int(pairs.h0[p]), t, q))
+
+
+def concat_bsw(parts):
+    """Concatenate BswPairs sets (offsets rebased)."""
+    tl = np.concatenate([p.tlen for p in parts])
+    ql = np.concatenate([p.qlen for p in parts])
+    toff = np.zeros(len(tl), np.int64)
+    qoff = np.zeros(len(ql), np.int64)
+    toff[1:] = np.cumsum(tl, dtype=np.int64)[:-1]
+    qoff[1:] = np.cumsum(ql, dtype=np.int64)[:-1]
+    return BswPairs(np.concatenate([p.tgt for p in parts]), toff, tl, np.concatenate([p.qry for p in parts]),
+                    qoff, ql, np.concatenate([p.h0 for p in parts]))
+
+
+BSW_LARGE_PAIRS = 10_606_460  # scripts/bsw_large:6 (SURVEY.md section 6)
+BSW_SMALL_PAIRS = 100_000     # scripts/bsw_outt:33
+
+
+def bsw_dataset(num_pairs: int = BSW_LARGE_PAIRS, seed: int = 11, threads: int = 16, chunk: int = 1 << 18):
+    """bsw_pairs at dataset scale: chunk c is bsw_pairs(chunk, seed=(seed, c)), generated on a thread
+    pool (numpy releases the GIL) and concatenated."""
+    from concurrent.futures import ThreadPoolExecutor
+    sizes = [min(chunk, num_pairs - o) for o in range(0, num_pairs, chunk)]
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        parts = list(ex.map(lambda a: bsw_pairs(a[1], seed=[seed, a[0]]), enumerate(sizes)))
+    return concat_bsw(parts) if parts else bsw_pairs(0, seed)

@@ -81,3 +81,23 @@ int64_t ref_bwa_collect(void *bwtp, const uint8_t *seq, int len, int min_seed_le
   free(t1.a);
   return cnt;
 }
+
+/* Banded SW extension: bwa v1 ksw_extend2 (tools/bwa/ksw.c:380-481), the function the bsw
+ * benchmark's scalarBandedSWA (benchmarks/bsw/bandedSWA.cpp:130-251) restates. ksw.c is compiled
+ * with -DNDEBUG so its h0 > 0 assert is off, matching the benchmark (bandedSWA.cpp:139).
+ * Same flattened layout as bsw_oracle_batch; out6 = {score, qle, tle, gtle, gscore, max_off}. */
+int ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore,
+                int *max_off);
+
+void ref_bwa_ksw_batch(int64_t n, const uint8_t *tgt, const int64_t *toff, const int32_t *tlen,
+                       const uint8_t *qry, const int64_t *qoff, const int32_t *qlen,
+                       const int32_t *h0, const int8_t *mat, const int32_t *params, int32_t *out) {
+  for (int64_t p = 0; p < n; ++p) {
+    int32_t *o = out + 6 * p;
+    o[0] = ksw_extend2(qlen[p], qry + qoff[p], tlen[p], tgt + toff[p], 5, mat, params[0],
+                       params[1], params[2], params[3], params[6], params[5], params[4], h0[p],
+                       &o[1], &o[2], &o[3], &o[4], &o[5]);
+  }
+}

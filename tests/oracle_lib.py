@@ -85,3 +85,51 @@ def ref_chain_run(lib, calls, nthreads=4):
                         calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data,
                         *[o.ctypes.data for o in out], nthreads)
     return [o[:n] for o in out]
+
+
+def _bsw_args(pairs, params):
+    import numpy as np
+    mat = np.ascontiguousarray(params.mat_array())
+    par = np.ascontiguousarray(params.as_array())
+    tgt = pairs.tgt if len(pairs.tgt) else np.zeros(1, np.uint8)
+    qry = pairs.qry if len(pairs.qry) else np.zeros(1, np.uint8)
+    keep = (mat, par, tgt, qry)
+    return keep, [pairs.n, tgt.ctypes.data, pairs.toff.ctypes.data, pairs.tlen.ctypes.data, qry.ctypes.data,
+                  pairs.qoff.ctypes.data, pairs.qlen.ctypes.data, pairs.h0.ctypes.data, mat.ctypes.data,
+                  par.ctypes.data]
+
+
+def bsw_oracle(pairs, params, nthreads=4):
+    """oracle/bsw_oracle.c over gen.BswPairs -> (out6 [n,6], cells [n], total cells)."""
+    import numpy as np
+    lib = oracle()
+    if not getattr(lib, "_bsw_decl", False):
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.bsw_oracle_batch.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        lib.bsw_oracle_batch.restype = ctypes.c_int64
+        lib._bsw_decl = True
+    out = np.zeros((max(pairs.n, 1), 6), np.int32)
+    cells = np.zeros(max(pairs.n, 1), np.int64)
+    keep, a = _bsw_args(pairs, params)
+    tot = lib.bsw_oracle_batch(*a, out.ctypes.data, cells.ctypes.data, nthreads)
+    return out[:pairs.n], cells[:pairs.n], tot
+
+
+def ref_bsw():
+    """bwa v1 ksw_extend2 compiled from the reference tree (oracle/_ref/libref_bwa.so) or None."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libref_bwa.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    lib.ref_bwa_ksw_batch.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.ref_bwa_ksw_batch.restype = None
+    return lib
+
+
+def ref_bsw_run(lib, pairs, params):
+    import numpy as np
+    out = np.zeros((max(pairs.n, 1), 6), np.int32)
+    keep, a = _bsw_args(pairs, params)
+    lib.ref_bwa_ksw_batch(*a, out.ctypes.data)
+    return out[:pairs.n]

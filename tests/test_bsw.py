@@ -1,0 +1,163 @@
+"""Banded SW parity. CPU: the C restatement (oracle/bsw_oracle.c) against the golden outputs of bwa v1
+ksw_extend2 -- the function the benchmark's scalarBandedSWA (bandedSWA.cpp:130-251) restates --
+(tests/golden/bsw_golden.npz, six parameter sets) and, when built, against ksw_extend2 live. GPU: the
+HIP kernel (csrc/bsw.hip) bit-exact on score/qle/tle/gtle/gscore/max_off and on the DP cell count."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from conftest import GOLDEN
+from genomicsbench_palisade_amd import bsw, gen
+
+FIELDS = bsw.OUT_FIELDS
+
+
+@pytest.fixture(scope="module")
+def golden():
+    z = np.load(os.path.join(GOLDEN, "bsw_golden.npz"))
+    p = gen.BswPairs(z["tgt"], z["toff"], z["tlen"], z["qry"], z["qoff"], z["qlen"], z["h0"])
+    sets = {}
+    for k in z.files:
+        if k.endswith("_out"):
+            name = k[:-4]
+            par = z[name + "_params"]
+            mat = z[name + "_mat"]
+            P = bsw.Params(*[int(v) for v in par])
+            for i in range(25):
+                P.mat[i] = int(mat[i])
+            sets[name] = (P, z[k])
+    return p, sets
+
+
+def assert_same(got, exp, what=""):
+    bad = np.nonzero((got != exp).any(axis=1))[0]
+    if len(bad):
+        b = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} pairs differ; first pair {b}: got "
+                             f"{dict(zip(FIELDS, got[b].tolist()))} expected {dict(zip(FIELDS, exp[b].tolist()))}")
+
+
+def test_params_match_benchmark_defaults():
+    p = bsw.default_params()
+    assert (p.o_del, p.e_del, p.o_ins, p.e_ins, p.zdrop, p.end_bonus, p.w) == (6, 1, 6, 1, 100, 5, 100)
+    m = p.mat_array().reshape(5, 5)
+    assert (np.diag(m)[:4] == 1).all() and m[0, 1] == -4 and (m[4] == -1).all() and (m[:, 4] == -1).all()
+
+
+def test_oracle_vs_golden(golden):
+    p, sets = golden
+    assert len(sets) == 6
+    for name, (P, exp) in sets.items():
+        got, cells, tot = oracle_lib.bsw_oracle(p, P)
+        assert_same(got, exp, name)
+        assert tot == cells.sum() > 0
+
+
+def test_oracle_vs_reference_live():
+    lib = oracle_lib.ref_bsw()
+    if lib is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    p = gen.bsw_pairs(20000, seed=123)
+    for kw in ({}, {"w": 3}, {"zdrop": 1}):
+        P = bsw.default_params(**kw)
+        assert_same(oracle_lib.bsw_oracle(p, P)[0], oracle_lib.ref_bsw_run(lib, p, P), str(kw))
+
+
+def test_pair_file_roundtrip(tmp_path):
+    """write_bsw_file emits the loadPairs format (main_banded.cpp:160-202): h0, ref, query lines."""
+    p = gen.bsw_pairs(50, seed=5)
+    f = tmp_path / "pairs.txt"
+    gen.write_bsw_file(f, p)
+    lines = f.read_bytes().split(b"\n")
+    assert len(lines) == 3 * p.n + 1 and lines[-1] == b""
+    for k in range(p.n):
+        assert int(lines[3 * k]) == p.h0[k]
+        t = np.frombuffer(lines[3 * k + 1], np.uint8) - 48
+        q = np.frombuffer(lines[3 * k + 2], np.uint8) - 48
+        assert (t == p.tgt[p.toff[k]:p.toff[k] + p.tlen[k]]).all()
+        assert (q == p.qry[p.qoff[k]:p.qoff[k] + p.qlen[k]]).all()
+
+
+def test_seqpair_layout():
+    assert bsw.SEQPAIR_DTYPE.itemsize == 72
+    assert ctypes.sizeof(bsw.Params) == 7 * 4 + 25 + 3
+
+
+# ---------------------------------------------------------------- GPU
+
+def _gpu(p, P):
+    from genomicsbench_palisade_amd import set_device
+    set_device(0)
+    b = bsw.BswBatch(p, P)
+    b.run()
+    out, cells, tot = b.results()
+    b.close()
+    return out, cells, tot
+
+
+@pytest.mark.gpu
+def test_gpu_vs_golden(golden):
+    p, sets = golden
+    for name, (P, exp) in sets.items():
+        got, cells, tot = _gpu(p, P)
+        assert_same(got, exp, name)
+        ocells = oracle_lib.bsw_oracle(p, P)[1]
+        assert (cells == ocells).all(), f"{name}: cell counts differ on {(cells != ocells).sum()} pairs"
+        assert tot == ocells.sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,qlen,extra", [(1, 100000, (10, 150), (0, 100)), (2, 20000, (150, 255), (0, 400)),
+                                               (3, 20000, (1, 70), (0, 1500))])
+def test_gpu_vs_oracle(seed, n, qlen, extra):
+    p = gen.bsw_pairs(n, seed=seed, qlen=qlen, extra=extra)
+    P = bsw.default_params()
+    got, cells, tot = _gpu(p, P)
+    exp, ocells, otot = oracle_lib.bsw_oracle(p, P, nthreads=8)
+    assert_same(got, exp, f"seed {seed}")
+    assert (cells == ocells).all() and tot == otot
+
+
+@pytest.mark.gpu
+def test_gpu_get_scores16_and_repeat():
+    from genomicsbench_palisade_amd import set_device
+    set_device(0)
+    p = gen.bsw_pairs(5000, seed=9)
+    P = bsw.default_params()
+    sp = bsw.get_scores16(p, P)
+    exp = oracle_lib.bsw_oracle(p, P)[0]
+    got = np.stack([sp[f] for f in FIELDS], axis=1)
+    assert_same(got, exp, "get_scores16")
+    assert (sp["id"] == np.arange(p.n)).all() and (sp["seqid"] == -1).all()
+    b = bsw.BswBatch(p, P)
+    outs = []
+    for _ in range(3):
+        b.run()
+        outs.append(b.results()[0])
+    assert all((o == outs[0]).all() for o in outs)
+    assert b.timing() > 0
+    b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_rejects_bad_pairs():
+    from genomicsbench_palisade_amd import GbError, set_device
+    set_device(0)
+    P = bsw.default_params()
+    for ql in (0, 256):
+        q = np.zeros(max(ql, 1), np.uint8)
+        p = gen.BswPairs(np.zeros(4, np.uint8), np.zeros(1, np.int64), np.array([4], np.int32), q,
+                         np.zeros(1, np.int64), np.array([ql], np.int32), np.array([10], np.int32))
+        with pytest.raises(GbError):
+            bsw.BswBatch(p, P)
+    p = gen.BswPairs(np.zeros(4, np.uint8), np.array([2], np.int64), np.array([4], np.int32), np.zeros(4, np.uint8),
+                     np.zeros(1, np.int64), np.array([4], np.int32), np.array([10], np.int32))
+    with pytest.raises(GbError):
+        bsw.BswBatch(p, P)
+    empty = gen.BswPairs(np.zeros(0, np.uint8), np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.uint8),
+                         np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32))
+    out, cells, tot = _gpu(empty, P)
+    assert out.shape == (0, 6) and tot == 0
