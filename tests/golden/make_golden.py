@@ -160,7 +160,7 @@ def bsw_inputs(seed=77):
     rng = np.random.default_rng(seed + 1)
     extra = []
     q = rng.integers(0, 4, 255).astype(np.uint8)
-    extra += [(q[:1], q[:1], 30), (q[:1], q[:5], 30), (q, q, 40), (q, np.concatenate([q, q[:50]]), 60),
+    extra += [(q[:1], q[:1], 30), (q[:1], q[:5], 30), (q, q, 40), (np.concatenate([q, q[:50]]), q, 60),
               (q[:200], q[:10], 70), (np.full(40, 4, np.uint8), np.full(30, 4, np.uint8), 25),
               (rng.integers(0, 4, 2046).astype(np.uint8), q[:10], 20), (q[:60], q[:60], 0), (q[:60], q[:60], 250),
               (rng.integers(0, 4, 300).astype(np.uint8), q[:150], 5)]
