@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <numeric>
 #include <vector>
@@ -42,6 +44,7 @@ struct Args {
   const int32_t *order;  // calls, longest first
   int32_t *score, *parent, *target, *peak;
   unsigned long long *visited;
+  unsigned long long *prof;  // optional phase clocks (GB_CHAIN_PROF=1): head, steps, tail, nsteps
 };
 
 __device__ __forceinline__ int ilog2_32(uint32_t v) { return 31 - __clz((int)v); }  // v > 0 (LogTable256)
@@ -53,6 +56,41 @@ __device__ __forceinline__ uint64_t dpp_shr_u64(uint64_t v, uint64_t lane0) {
   const int lo = dpp_shr_i32((int)(uint32_t)v, (int)(uint32_t)lane0);
   const int hi = dpp_shr_i32((int)(uint32_t)(v >> 32), (int)(uint32_t)(lane0 >> 32));
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+constexpr int32_t kNegB = -(1 << 28);
+
+// anchors are read-only for the whole kernel: the constant address space turns the uniform X[st]
+// reads of the window-start loop into scalar loads (lgkmcnt), so they never wait behind the
+// wave's outstanding score/parent/peak stores (vmcnt)
+typedef const __attribute__((address_space(4))) uint64_t const_u64;  // identity of the n_skip composition scan
+
+// wave-wide inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
+__device__ __forceinline__ int32_t scan_max(int32_t v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xA, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xC, 0xF, false));
+  return v;
+}
+// (a, b) represents n -> max(n + a, b); earlier lanes apply first: (a1,b1) then (a2,b2) =
+// (a1 + a2, max(b1 + a2, b2)). Identity (0, kNegB).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void compose_step(int32_t &a, int32_t &b) {
+  const int32_t ua = __builtin_amdgcn_update_dpp(0, a, CTRL, ROWS, 0xF, false);
+  const int32_t ub = __builtin_amdgcn_update_dpp(kNegB, b, CTRL, ROWS, 0xF, false);
+  b = max(ub + a, b);
+  a = ua + a;
+}
+__device__ __forceinline__ void scan_compose(int32_t &a, int32_t &b) {
+  compose_step<0x111, 0xF>(a, b);
+  compose_step<0x112, 0xF>(a, b);
+  compose_step<0x114, 0xF>(a, b);
+  compose_step<0x118, 0xF>(a, b);
+  compose_step<0x142, 0xA>(a, b);
+  compose_step<0x143, 0xC>(a, b);
 }
 
 __device__ __forceinline__ int32_t load_l2(const int32_t *p) {
@@ -69,6 +107,7 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
   const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
   const double avg_qspan = (double)A.avg_qspan[c];
   const uint64_t *X = A.x + o, *Y = A.y + o;
+  const const_u64 *XC = (const const_u64 *)X, *YC = (const const_u64 *)Y;
   int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
 
   for (int k = lane; k < kRing; k += 64) S[k] = 0;
@@ -83,8 +122,10 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
   int32_t ps = 0, pp = -1, pk = 0;
   int64_t st = 0;
   unsigned long long vis = 0;
-
+  unsigned long long c_head = 0, c_step = 0, c_tail = 0, n_step = 0, t_0 = 0, t_1 = 0;
+  const bool prof = A.prof != nullptr;
   for (int64_t i = 0; i < n; i++) {
+    if (prof) t_0 = __builtin_amdgcn_s_memtime();
     if (i > 0) {
       wx = dpp_shr_u64(wx, px);
       wy = dpp_shr_u64(wy, py);
@@ -93,16 +134,22 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
       wpk = dpp_shr_i32(wpk, pk);
     }
     if ((i & 31) == 0) __builtin_amdgcn_s_waitcnt(0);  // stores of steps <= i-32 are in L2
-    const uint64_t xi = X[i], yi = Y[i];
+    const uint64_t xi = XC[i], yi = YC[i];  // scalar loads
     const int32_t qi = (int32_t)yi, q_span = (int32_t)(yi >> 32 & 0xff);
     const int32_t sidi = (int32_t)((yi & (0xffull << 48)) >> 48);
-    while (st < i && xi > X[st] + (uint64_t)(int64_t)max_dist_x) ++st;
+    while (st < i && xi > XC[st] + (uint64_t)(int64_t)max_dist_x) ++st;
     if (i - st > kMaxIter) st = i - kMaxIter;
 
     int32_t M = q_span, N = 0;
     int64_t J = -1;
     const uint32_t stamp = (uint32_t)(i + 1);
+    if (prof) {
+      t_1 = __builtin_amdgcn_s_memtime();
+      c_head += t_1 - t_0;
+      t_0 = t_1;
+    }
     for (int64_t jtop = i - 1; jtop >= st; jtop -= 64) {
+      if (prof) ++n_step;
       const int64_t j = jtop - lane;
       const bool valid = j >= st;
       uint64_t xj, yj;
@@ -156,25 +203,11 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
       if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
       const bool tgt = valid && S[j & (kRing - 1)] == stamp;
       // ---- sequential order as prefix scans over lanes ---------------------------------------
-      int32_t mx = ok ? sc : INT_MIN;  // inclusive max scan
-      int32_t a = 0, b = 0;            // n -> max(n + a, b)
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t u = __shfl_up(mx, d);
-        if (lane >= d) mx = max(mx, u);
-      }
-      int32_t before = __shfl_up(mx, 1);
-      if (lane == 0) before = INT_MIN;
-      before = max(before, M);
+      int32_t mx = scan_max(ok ? sc : INT_MIN);  // inclusive max scan
+      const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
       const bool upd = ok && sc > before;
-      a = upd ? -1 : ((ok && tgt) ? 1 : 0);
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t ua = __shfl_up(a, d), ub = __shfl_up(b, d);
-        if (lane >= d) {
-          const int32_t na = ua + a, nb = max(ub + a, b);
-          a = na;
-          b = nb;
-        }
-      }
+      int32_t a = upd ? -1 : ((ok && tgt) ? 1 : 0), b = 0;  // n -> max(n + a, b); n >= 0 always
+      scan_compose(a, b);
       const int32_t n_after = max(N + a, b);
       const bool brk = ok && !upd && tgt && n_after > kMaxSkip;
       const uint64_t bm = __ballot(brk);
@@ -187,20 +220,31 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
       if (um) {
         const int lu = 63 - __builtin_clzll(um);
         J = jtop - lu;
-        M = __shfl(mx, lu);
+        M = __builtin_amdgcn_readlane(mx, lu);
       }
       if (ok && lane < bl && pj >= 0) target[pj] = (int32_t)i;
       if (bl < 64) break;
-      N = __shfl(n_after, 63);
+      N = __builtin_amdgcn_readlane(n_after, 63);
+    }
+    if (prof) {
+      t_1 = __builtin_amdgcn_s_memtime();
+      c_step += t_1 - t_0;
+      t_0 = t_1;
     }
     int32_t pkJ = 0;
-    if (J >= 0) pkJ = (J >= i - 64) ? __shfl(wpk, (int)(i - 1 - J)) : load_l2(peak + J);
+    if (J >= 0) {
+      if (J >= i - 64)
+        pkJ = __builtin_amdgcn_readlane(wpk, (int)(i - 1 - J));
+      else  // rare: consume the load inside the branch so the common path carries no vmcnt wait
+        pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
+    }
     const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
     if (lane == 0) {
       score[i] = M;
       parent[i] = (int32_t)J;
       peak[i] = pki;
     }
+    if (prof) c_tail += __builtin_amdgcn_s_memtime() - t_0;
     px = xi;
     py = yi;
     ps = M;
@@ -208,6 +252,12 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
     pk = pki;
   }
   // wave-reduce the visited count
+  if (prof && lane == 0) {
+    atomicAdd(A.prof + 0, c_head);
+    atomicAdd(A.prof + 1, c_step);
+    atomicAdd(A.prof + 2, c_tail);
+    atomicAdd(A.prof + 3, n_step);
+  }
   for (int d = 32; d >= 1; d >>= 1) vis += __shfl_xor(vis, d);
   if (lane == 0) atomicAdd(A.visited, vis / 64);
 }
@@ -225,6 +275,7 @@ struct gb_chain_batch {
   uint64_t *d_x = nullptr, *d_y = nullptr;
   int32_t *d_out = nullptr;  // score | parent | target | peak
   unsigned long long *d_vis = nullptr;
+  unsigned long long *d_prof = nullptr;  // GB_CHAIN_PROF=1 phase clocks (development aid)
   bool ran = false;
 };
 
@@ -298,10 +349,24 @@ int gb_chain_batch_run(gb_chain_batch *B) {
     A.target = B->d_out + 2 * nn;
     A.peak = B->d_out + 3 * nn;
     A.visited = B->d_vis;
+    A.prof = nullptr;
+    const char *pe = getenv("GB_CHAIN_PROF");
+    if (pe && *pe == '1') {
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 4 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 4 * sizeof(unsigned long long), B->stream));
+      A.prof = B->d_prof;
+    }
     hipLaunchKernelGGL(gbchain::chain_kernel, dim3((unsigned)B->ncalls), dim3(64), 0, B->stream, A);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
+  if (B->d_prof && getenv("GB_CHAIN_PROF")) {
+    unsigned long long h[4];
+    GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
+    GB_HIP(hipStreamSynchronize(B->stream));
+    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu\n", h[0], h[1],
+            h[2], h[3]);
+  }
   B->ran = true;
   return GB_OK;
 }
@@ -342,7 +407,7 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
   if (!B) return GB_OK;
   if (B->stream) (void)hipStreamSynchronize(B->stream);
   for (void *p : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order, (void *)B->d_x,
-                  (void *)B->d_y, (void *)B->d_out, (void *)B->d_vis})
+                  (void *)B->d_y, (void *)B->d_out, (void *)B->d_vis, (void *)B->d_prof})
     (void)hipFree(p);
   for (auto ev : B->ev)
     if (ev) (void)hipEventDestroy(ev);
