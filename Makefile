@@ -18,7 +18,8 @@ HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(LIB)/obj/%.o,$(HIP_SRCS)) $(LIB)/obj/gb_c
 HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
 .PHONY: all ref clean oracle
-all: $(LIB)/libgb.so $(LIB)/libgkl_pairhmm_c.so $(BIN)/phmm oracle
+DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so
+all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw oracle
 
 $(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIB)/obj
@@ -35,6 +36,18 @@ $(LIB)/libgb.so: $(HIP_OBJS)
 # C++ linkage (IntelPairHmmCSource.cpp:29-115) on top of libgb.so.
 $(LIB)/libgkl_pairhmm_c.so: $(CSRC)/gkl_dropin.cpp $(LIB)/libgb.so $(HDRS)
 	$(HOSTCXX) $(HOSTFLAGS) -shared -o $@ $< -L$(LIB) -lgb -Wl,-rpath,'$$ORIGIN'
+
+# host_chain_kernel (C++ linkage, gb_compat/minimap2_chain.h) and BandedPairWiseSW (gb_compat/bandedSWA.h)
+$(LIB)/libgb_%_dropin.so: $(CSRC)/%_dropin.cpp $(LIB)/libgb.so $(HDRS) $(wildcard include/gb_compat/*.h)
+	$(HOSTCXX) $(HOSTFLAGS) -shared -o $@ $< -L$(LIB) -lgb -Wl,-rpath,'$$ORIGIN'
+
+$(BIN)/chain: $(PKG)/drivers/chain_main.cpp $(LIB)/libgb_chain_dropin.so
+	@mkdir -p $(BIN)
+	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb_chain_dropin -lgb -Wl,-rpath,'$$ORIGIN/../lib'
+
+$(BIN)/bsw: $(PKG)/drivers/bsw_main.cpp $(LIB)/libgb_bsw_dropin.so
+	@mkdir -p $(BIN)
+	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb_bsw_dropin -lgb -Wl,-rpath,'$$ORIGIN/../lib'
 
 $(BIN)/phmm: $(PKG)/drivers/phmm_main.cpp $(LIB)/libgb.so
 	@mkdir -p $(BIN)

@@ -161,3 +161,22 @@ def test_gpu_rejects_bad_pairs():
                          np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32))
     out, cells, tot = _gpu(empty, P)
     assert out.shape == (0, 6) and tot == 0
+
+
+@pytest.mark.gpu
+def test_gpu_cli_dropin(golden, tmp_path):
+    """bin/bsw (CLI of main_banded.cpp over BandedPairWiseSW::getScores16 from libgb_bsw_dropin.so)
+    on a loadPairs-format file reproduces ksw_extend2's outputs."""
+    import subprocess
+    from conftest import ROOT
+    p, sets = golden
+    P, exp = sets["default"]
+    fin, fout = tmp_path / "pairs.txt", tmp_path / "out.tsv"
+    gen.write_bsw_file(fin, p)
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "bsw")
+    r = subprocess.run([exe, "-pairs", str(fin), "-t", "1", "-b", "512", "-o", str(fout)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert f"Total Pairs processed: {p.n}" in r.stdout
+    got = np.loadtxt(fout, dtype=np.int32, ndmin=2)
+    assert_same(got, exp, "bsw CLI")

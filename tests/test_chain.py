@@ -70,3 +70,29 @@ def test_gpu_vs_oracle(seed, ncalls, median, maxn):
     b.run()
     assert_same(b.results(), exp)  # re-run on the same device buffers
     b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_cli_dropin(golden, tmp_path):
+    """bin/chain (CLI of minimap2-acceleration kernel/scalar main.cpp over host_chain_kernel from
+    libgb_chain_dropin.so): read_call input -> print_return output equal to the reference's."""
+    import subprocess
+    from conftest import ROOT
+    calls, exp = golden
+    fin, fout = tmp_path / "in.txt", tmp_path / "out.txt"
+    gen.write_chain_file(fin, calls)
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "chain")
+    r = subprocess.run([exe, "-i", str(fin), "-o", str(fout), "-t", "4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Time in kernel" in r.stderr
+    toks = fout.read_text().split("EOR\n")
+    assert toks[-1] == "" and len(toks) == calls.ncalls + 1
+    sc, par = [], []
+    for c, blk in enumerate(toks[:-1]):
+        lines = blk.strip("\n").split("\n")
+        assert int(lines[0]) == calls.offsets[c + 1] - calls.offsets[c]
+        for ln in lines[1:]:
+            a, b = ln.split("\t")
+            sc.append(int(a))
+            par.append(int(b))
+    assert (np.array(sc) == exp[0]).all() and (np.array(par) == exp[1]).all()
