@@ -43,6 +43,24 @@ BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar in
 PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
+def pmc_traffic(kernel: str):
+    """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE) of `kernel` from the newest committed
+    profiles/*_pmc.json (rocprofv3 PMC passes of this same bench configuration, tools/gpu_prof.sh +
+    tools/pmc_summary.py); None when no profile covers it. PMC cannot run inside the timed process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if kernel in d:
+            return {"bytes": d[kernel]["fetch_bytes"] + d[kernel]["write_bytes"],
+                    "fetch_bytes": d[kernel]["fetch_bytes"], "write_bytes": d[kernel]["write_bytes"],
+                    "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -285,7 +303,7 @@ def bench_chain(args, D, rank, world):
                                f"n, median 1500, max 87271), max_dist 5000, bw 500, n_segs 1",
                    "visited_pairs": int(visited), "gpairs_per_s": visited * args.steps * D.world / elapsed / 1e9},
         "roofline": {"bound": "valu", "kernel": "chain_kernel", "achieved": ach / 1e12, "peak": PEAK_CHAIN_OPS / 1e12,
-                     "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": None,
+                     "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": pmc_traffic("chain_kernel"),
                      "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_kernel": ms},
         "cpu_baseline": cpu,
@@ -328,7 +346,7 @@ def bench_bsw(args, D, rank, world):
                    "cells": int(cells), "mpairs_per_s": pairs.n * D.world * args.steps / elapsed / 1e6},
         "roofline": {"bound": "valu", "kernel": "bsw_extend_kernel", "achieved": ach / 1e12,
                      "peak": PEAK_INT_OPS / 1e12, "unit": "T int op/s", "frac": ach / PEAK_INT_OPS,
-                     "traffic": None, "ops_per_cell": BSW_OPS_PER_CELL},
+                     "traffic": pmc_traffic("bsw_extend_kernel"), "ops_per_cell": BSW_OPS_PER_CELL},
         "kernels_ms": {"bsw_extend_kernel": ms},
         "cpu_baseline": cpu,
     }
@@ -381,7 +399,7 @@ def bench_phmm(args, D, rank, world):
     return {
         "value": gcups, "elapsed": elapsed, "ntc": ntc, "cells": cells, "f64_frac": float(used.mean()),
         "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
-                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": None},
+                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": pmc_traffic(kern)},
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
         "cpu_baseline": cpu,
     }
@@ -439,7 +457,7 @@ def bench_fmi(args, D, rank, world):
                    "smems_per_read": total / len(lens), "num_smem1_2_3": [int(x) for x in phases],
                    "backwardExt_per_read": calls / len(lens), "index_build_s": round(t_index, 2)},
         "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
-                     "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": None,
+                     "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": pmc_traffic("smem_search"),
                      "algorithmic_bytes": int(alg_bytes)},
         "kernels_ms": {"smem_search": ms, "smem_search+scan": float(np.mean(kt))},
         "cpu_baseline": cpu,

@@ -1,0 +1,54 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/<tag>_pmc.json:
+per hot kernel (fmi pass 1 and pass 2 told apart by grid size) the mean duration, FETCH_SIZE and
+WRITE_SIZE per launch converted from KiB to bytes. No correction factor is applied: the gfx950 x2
+FETCH_SIZE correction of MI355X_MICROARCH.md is calibrated for wide coalesced streaming reads only.
+
+    python tools/pmc_summary.py gpurun_out/pmc_fetch_TAG gpurun_out/pmc_write_TAG profiles/TAG_pmc.json
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
+       "smem_search": "smem_search", "chain_kernel": "chain_kernel", "bsw_extend_kernel": "bsw_extend_kernel"}
+
+
+def name_of(r):
+    for k, v in HOT.items():
+        if k in r["Kernel_Name"].replace(", ", "<").replace("(", "<"):
+            if v == "smem_search" and int(r["Grid_Size"]) <= 4096:
+                return "smem_search(pass 2)"
+            return v
+    return None
+
+
+def load(d):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        n = name_of(r)
+        if n:
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+            out[n].append((float(r["Counter_Value"]) * 1024.0, dur))
+    return out
+
+
+def main():
+    fetch, write, dst = sys.argv[1], sys.argv[2], sys.argv[3]
+    f, w = load(fetch), load(write)
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        fb = [v for v, _ in f.get(k, [])]
+        wb = [v for v, _ in w.get(k, [])]
+        ms = [d for _, d in f.get(k, [])] + [d for _, d in w.get(k, [])]
+        res[k] = {"launches": len(fb), "fetch_bytes": sum(fb) / max(len(fb), 1),
+                  "write_bytes": sum(wb) / max(len(wb), 1), "mean_ms_under_pmc": sum(ms) / max(len(ms), 1)}
+    res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch, "
+                    "uncorrected (MI355X_MICROARCH.md HBM section)")
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
