@@ -19,7 +19,7 @@ HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
 .PHONY: all ref clean oracle
 DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so
-all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw oracle
+all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle
 
 $(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIB)/obj
@@ -48,6 +48,10 @@ $(BIN)/chain: $(PKG)/drivers/chain_main.cpp $(LIB)/libgb_chain_dropin.so
 $(BIN)/bsw: $(PKG)/drivers/bsw_main.cpp $(LIB)/libgb_bsw_dropin.so
 	@mkdir -p $(BIN)
 	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb_bsw_dropin -lgb -Wl,-rpath,'$$ORIGIN/../lib'
+
+$(BIN)/fmi: $(PKG)/drivers/fmi_main.cpp $(LIB)/libgb.so
+	@mkdir -p $(BIN)
+	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb -lz -Wl,-rpath,'$$ORIGIN/../lib'
 
 $(BIN)/phmm: $(PKG)/drivers/phmm_main.cpp $(LIB)/libgb.so
 	@mkdir -p $(BIN)

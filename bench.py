@@ -225,12 +225,15 @@ def cpu_baseline_chain(calls, sample_seconds: float):
     cum = np.cumsum((calls.offsets[order + 1] - calls.offsets[order]))
     m = int(min(calls.ncalls, max(64, np.searchsorted(cum, rate * sample_seconds))))
     s_ = sub(order[:m])
-    t = run(s_)
+    t1 = run(s_)  # the whole set can be shorter than the sample budget: repeat it
+    reps = max(1, int(sample_seconds / max(t1, 1e-6)))
+    t = t1 + sum(run(s_) for _ in range(reps - 1))
+    t /= reps
     return {"value": s_.nanchors / t / 1e6, "unit": "Manchors/s", "cores": threads,
             "kind": "reference" if ref is not None else "port",
             "sample": f"{m} of {calls.ncalls} calls ({s_.nanchors} anchors, random) of the same set, "
                       f"{'minimap2-acceleration scalar chain_dp' if ref is not None else 'C restatement'}, "
-                      f"OpenMP {threads} threads, {t:.1f} s"}
+                      f"OpenMP {threads} threads, {reps} pass(es) of {t:.2f} s"}
 
 
 def cpu_baseline_bsw(pairs, params, sample_seconds: float):

@@ -287,17 +287,14 @@ void gb_bsw_default_params(gb_bsw_params *p) {
 
 int gb_bsw_batch_destroy(gb_bsw_batch *B) {
   if (!B) return GB_OK;
-  if (B->device >= 0) hipSetDevice(B->device);
-  if (B->stream) hipStreamSynchronize(B->stream);
-  hipFree(B->d_pairs);
-  hipFree(B->d_tgt);
-  hipFree(B->d_qry);
-  hipFree(B->d_out6);
-  hipFree(B->d_cells);
-  hipFree(B->d_total);
+  if (B->device >= 0) (void)hipSetDevice(B->device);
+  if (B->stream) (void)hipStreamSynchronize(B->stream);
+  for (void *p : {(void *)B->d_pairs, (void *)B->d_tgt, (void *)B->d_qry, (void *)B->d_out6, (void *)B->d_cells,
+                  (void *)B->d_total})
+    (void)hipFree(p);
   for (auto &e : B->ev)
-    if (e) hipEventDestroy(e);
-  if (B->stream) hipStreamDestroy(B->stream);
+    if (e) (void)hipEventDestroy(e);
+  if (B->stream) (void)hipStreamDestroy(B->stream);
   delete B;
   return GB_OK;
 }

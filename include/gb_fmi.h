@@ -10,8 +10,8 @@
  *     sortSMEMs(...)                                                FMI_search.cpp:1520-1534
  *     build_index()                                                 FMI_search.cpp:358-434
  *   driven per batch by benchmarks/fmi/fmi.cpp:253-348 (smem1 -> reseed -> LAST -> rid offset -> sort).
- * gb_fmi_search() runs that whole per-batch pipeline for every read on the GPU; the per-method entry
- * points serve the FMI_search adapter (include/fmi_search_gpu.h) one call at a time.
+ * gb_fmi_search() runs that whole per-batch pipeline for every read on the GPU (the CLI drop-in is
+ * drivers/fmi_main.cpp -> bin/fmi).
  *
  * Plain pointers and sizes; 0 on success, negative gb_status on failure (gb_last_error()).
  */

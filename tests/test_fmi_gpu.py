@@ -121,3 +121,35 @@ def test_overflow_second_pass(fmi):
     assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
     assert (bc == ebc).all() and (pc == epc).all()
     assert rs.timing()[2] == oi.bwt_calls()
+
+
+def test_cli_dropin(fmi, golden, tmp_path):
+    """bin/fmi (CLI of benchmarks/fmi/fmi.cpp: index prefix, FASTQ, batch size, minSeedLen, threads)
+    with GB_FMI_PRINT_OUTPUT=1 prints the same SMEMs and per-batch totals as bwa on the golden set."""
+    import subprocess
+    from conftest import ROOT
+    prefix = str(tmp_path / "ref.fa")
+    fmi.Index.build(golden["ref"], out_path=prefix + ".bwt.2bit.64").close()
+    fq = tmp_path / "reads.fq"
+    gen.write_fastq(fq, golden["codes"], golden["lens"])
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "fmi")
+    env = dict(os.environ, GB_FMI_PRINT_OUTPUT="1")
+    r = subprocess.run([exe, prefix, str(fq), "64", "19", "1"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout[-2000:]
+    got, rid = [], -1
+    batches = {}
+    for ln in r.stdout.splitlines():
+        if ln.startswith("batch_id: "):
+            b, c = ln[len("batch_id: "):].split(", numTotalSmem[batch_id]: ")
+            batches[int(b)] = int(c)
+        elif ln.startswith("totalSmems = "):
+            total = int(ln.split("=")[1])
+        elif ln.endswith(":") and ln[:-1].isdigit():
+            rid = int(ln[:-1])
+        elif ln.startswith("[") and ln.endswith("]"):
+            m, n1 = ln[1:-1].split(",")
+            got.append((rid, int(m), int(n1) - 1))
+    exp = sorted(zip(golden["rid"].tolist(), golden["m"].tolist(), golden["n"].tolist()))
+    assert sorted(got) == exp
+    assert total == len(exp) and sum(batches.values()) == total
+    assert len(batches) == (len(golden["lens"]) + 63) // 64
