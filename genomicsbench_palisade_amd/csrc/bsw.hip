@@ -18,6 +18,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -40,7 +42,8 @@ struct Pair {  // device descriptor, 32 B
 
 struct Args {
   const Pair *pairs;
-  int64_t n;
+  const uint32_t *list;  // pair indices this launch processes
+  int64_t n;             // entries in list
   const uint8_t *tgt, *qry;
   int32_t *out6, *cells;
   unsigned long long *total_cells;
@@ -220,6 +223,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void bsw_extend_kernel(Args A)
     if (lane == 0) p = atomicAdd(A.next, 1u);
     p = __builtin_amdgcn_readfirstlane(p);
     if ((int64_t)p >= A.n) break;
+    p = A.list[p];
     const Pair P = A.pairs[p];
     int nc = 0;
     int32_t *o6 = A.out6 + 6 * (int64_t)p;
@@ -238,6 +242,229 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void bsw_extend_kernel(Args A)
   if (lane == 0 && wave_cells) atomicAdd(A.total_cells, wave_cells);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Pair-per-lane kernel (the reference's own inter-pair SIMD shape, getScores16): 64 pairs per wave,
+// each lane runs scalarBandedSWA for its pair. The lane's eh[0..qlen] lives in VGPRs, one register
+// per column packing h (bits 0-15) and e (bits 16-31), so every column index is a compile-time
+// constant: columns are swept in lockstep over the union of the lanes' bands, each lane's own band
+// [beg, end) selected by the EXEC mask, 8-column chunks outside every band skipped by a uniform
+// branch. Pairs are grouped by query length (NCH chunks of 8 columns hold eh[0..8*NCH-1]) and
+// sorted by target length so the 64 lanes of a wave run rows in near lockstep.
+// Exactness notes: M = H ? H + S : 0 only matters through max(M, 0) (h = max(M, e, f) with
+// e, f >= 0, and both gap openings clamp at 0), so M is formed as med3(H << 16, H + S, 0); all
+// scores stay below 2^15 (checked on the host), so the 16-bit packing is lossless.
+
+constexpr int kBias = 128;  // score bytes are stored biased (unsigned) for v_perm lookups
+
+struct LaneArgs {
+  const Pair *pairs;
+  const uint32_t *order;
+  int64_t first, count;  // order[first .. first+count)
+  const uint8_t *tgt, *qry;
+  int32_t *out6, *cells;
+  unsigned long long *total_cells;
+  int o_del, e_del, o_ins, e_ins, zdrop;
+  unsigned long long *prof;  // GB_BSW_PROF=1: {wave rows, chunk-columns swept, lane-rows active, cells}
+  uint32_t tab[10];  // per target code t: biased scores of query codes 0..3 (tab[2t]) and 4 (tab[2t+1])
+};
+
+template <int NCH>
+__global__ __launch_bounds__(64) void bsw_lane_kernel(LaneArgs A) {
+  constexpr int NCOL = 8 * NCH;
+  constexpr int NW = (NCOL + 31) / 32;
+  const int lane = threadIdx.x;
+  const int64_t k = A.first + (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = k < A.first + A.count;
+  const uint32_t p = valid ? A.order[k] : 0u;
+  Pair P;
+  if (valid) {
+    P = A.pairs[p];
+  } else {
+    P.t_off = P.q_off = 0;
+    P.tlen = 0;
+    P.qlen = 1;
+    P.h0 = 0;
+    P.w = 0;
+  }
+  const int qlen = P.qlen, tlen = P.tlen, h0 = P.h0, w = P.w;
+  const int o_del = A.o_del, e_del = A.e_del, o_ins = A.o_ins, e_ins = A.e_ins;
+  const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+  const uint8_t *qry = A.qry + P.q_off;
+  const uint8_t *tgt = A.tgt + P.t_off;
+
+  // query codes, 4 bits per column, 8 columns per word, staged in LDS (Qs[c][lane]) so they cost
+  // no VGPRs; eh row 0 (bandedSWA.cpp:157-159) computed in registers
+  __shared__ uint32_t Qs[NCH][64];
+  uint32_t X[NCOL];
+  const int v1 = max(h0 - oe_ins, 0);
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    uint32_t q = 0;
+    const int j0 = 8 * c;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint32_t code = j0 + b < qlen ? min((uint32_t)qry[j0 + b], 4u) : 4u;
+      q |= code << (4 * b);
+    }
+    Qs[c][lane] = q;
+  }
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j)
+    X[j] = j == 0 ? (uint32_t)h0 : (j <= qlen ? (uint32_t)max(v1 - (j - 1) * e_ins, 0) : 0u);
+
+  int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+  int ncells = 0;
+  bool active = valid && tlen > 0;
+  unsigned long long pr_rows = 0, pr_cols = 0, pr_lrows = 0;
+  // target bases: four rows per register; the next four are loaded one group ahead as independent
+  // byte loads (clamped in-bounds, never waited on until they are combined four rows later)
+  const int tmax = max(tlen - 1, 0);
+  uint32_t tcur = 0, tn[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) tcur |= (uint32_t)tgt[min(b, tmax)] << (8 * b);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) tn[b] = tgt[min(4 + b, tmax)];
+
+#pragma unroll 1
+  for (int i = 0;; ++i) {
+    if (i >= tlen) active = false;
+    if (__builtin_amdgcn_ballot_w64(active) == 0) break;
+    if (i > 0 && (i & 3) == 0) {
+      tcur = tn[0] | tn[1] << 8 | tn[2] << 16 | tn[3] << 24;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) tn[b] = tgt[min(i + 4 + b, tmax)];
+    }
+    const uint32_t tb = min((tcur >> (8 * (i & 3))) & 0xFFu, 4u);
+    uint32_t tlo = A.tab[8], thi = A.tab[9];  // per-lane row of the score table (select chain, no scratch)
+#pragma unroll
+    for (int t = 3; t >= 0; --t)
+      if (tb == (uint32_t)t) {
+        tlo = A.tab[2 * t];
+        thi = A.tab[2 * t + 1];
+      }
+    // band (bandedSWA.cpp:180-182)
+    if (beg < i - w) beg = i - w;
+    if (end > i + w + 1) end = i + w + 1;
+    if (end > qlen) end = qlen;
+    const int width = active ? max(end - beg, 0) : 0;
+    ncells += width;
+    if (A.prof) {
+      ++pr_rows;
+      pr_lrows += active ? 1 : 0;
+    }
+    int h1 = beg == 0 ? max(h0 - (o_del + e_del * (i + 1)), 0) : 0;
+    int f = 0, mkey = -1;
+    uint32_t nz[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) nz[q] = 0;
+    uint32_t qn = Qs[0][lane];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const uint32_t qc = qn;
+      if (c + 1 < NCH) qn = Qs[c + 1][lane];  // prefetch the next chunk's codes
+      // skip the chunk when it meets no lane's band
+      if (__builtin_amdgcn_ballot_w64(width > 0 && beg < 8 * c + 8 && end > 8 * c) == 0) continue;
+      if (A.prof) pr_cols += 8;
+      const uint32_t qe = qc & 0x0F0F0F0Fu, qo = (qc >> 4) & 0x0F0F0F0Fu;
+      const uint32_t se = __builtin_amdgcn_perm(thi, tlo, qe);  // biased scores, columns 0,2,4,6
+      const uint32_t so = __builtin_amdgcn_perm(thi, tlo, qo);  // columns 1,3,5,7
+      // branch-free: every lane evaluates all 8 columns (one basic block, so the scheduler can overlap
+      // column j+1's independent work with column j's f/h1 chain); out-of-band lanes keep their state
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int j = 8 * c + b;
+        // lane mask of the band, used as a bit-select (kept arithmetic so no branches come back)
+        const uint32_t msk = (uint32_t)(j - beg) < (uint32_t)width ? 0xFFFFFFFFu : 0u;
+        const uint32_t x = X[j];
+        const uint32_t sb = ((b & 1) ? so : se) >> (8 * (b >> 1)) & 0xFFu;
+        const int y = __builtin_amdgcn_sbfe((int)(x + sb - kBias), 0, 16);  // H + S
+        const int M = max(min((int)(x << 16), y), 0);                        // H ? H + S : 0 (clamped)
+        const int e = (int)(x >> 16);
+        const int h = max(max(M, e), f);
+        const int en = max(max(e - e_del, M - oe_del), 0);                    // E(i+1,j)
+        const int fn = max(max(f - e_ins, M - oe_ins), 0);                    // F(i,j+1)
+        const uint32_t xn = ((uint32_t)en << 16) | (uint32_t)h1;             // eh[j] = {H(i,j-1), E}
+        mkey = max(mkey, (int)((((uint32_t)h << 8 | (uint32_t)j) & msk) | ~msk));  // last argmax
+        nz[j >> 5] |= (min(xn, 1u) & msk) << (j & 31);
+        X[j] = (xn & msk) | (x & ~msk);
+        f = (int)(((uint32_t)fn & msk) | ((uint32_t)f & ~msk));
+        h1 = (int)(((uint32_t)h & msk) | ((uint32_t)h1 & ~msk));
+      }
+    }
+    // eh[end] = {h1, 0} (bandedSWA.cpp:217), chunks holding no lane's end skipped
+    const bool wend = active && end < NCOL;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (__builtin_amdgcn_ballot_w64(wend && (end >> 3) == c) == 0) continue;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int j = 8 * c + b;
+        if (wend && end == j) {
+          X[j] = (uint32_t)h1;
+          nz[j >> 5] = (nz[j >> 5] & ~(1u << (j & 31))) | (min((uint32_t)h1, 1u) << (j & 31));
+        }
+      }
+    }
+    if (!active) continue;
+    const int m = mkey < 0 ? 0 : (mkey >> 8);
+    const int mj = mkey < 0 ? -1 : (mkey & 0xFF);
+    if ((beg < end ? end : beg) == qlen) {  // bandedSWA.cpp:218-221
+      max_ie = gscore > h1 ? max_ie : i;
+      gscore = gscore > h1 ? gscore : h1;
+    }
+    if (m == 0) {
+      active = false;
+      continue;
+    }
+    if (m > mx) {
+      mx = m, max_i = i, max_j = mj;
+      max_off = max(max_off, abs(mj - i));
+    } else if (A.zdrop > 0) {
+      const bool brk = (i - max_i > mj - max_j) ? (mx - m - ((i - max_i) - (mj - max_j)) * e_del > A.zdrop)
+                                                : (mx - m - ((mj - max_j) - (i - max_i)) * e_ins > A.zdrop);
+      if (brk) {
+        active = false;
+        continue;
+      }
+    }
+    // band narrowing (bandedSWA.cpp:235-239): first nonzero eh in [beg, end), last in [beg', end]
+    int first = INT_MAX, last = -1;
+#pragma unroll
+    for (int q = NW - 1; q >= 0; --q)
+      if (nz[q]) first = 32 * q + __builtin_ctz(nz[q]);
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+      if (nz[q]) last = 32 * q + 31 - __builtin_clz(nz[q]);
+    const int nb = min(first, end);
+    const int je = last >= nb ? last : nb - 1;
+    beg = nb;
+    end = je + 2 < qlen ? je + 2 : qlen;
+  }
+  if (valid) {
+    int32_t *o6 = A.out6 + 6 * (int64_t)p;
+    o6[0] = mx;
+    o6[1] = max_j + 1;
+    o6[2] = max_i + 1;
+    o6[3] = max_ie + 1;
+    o6[4] = gscore;
+    o6[5] = max_off;
+    A.cells[p] = ncells;
+  }
+  unsigned long long wc = (unsigned long long)ncells;
+  for (int d = 32; d >= 1; d >>= 1) wc += __shfl_xor(wc, d);
+  if (lane == 0 && wc) atomicAdd(A.total_cells, wc);
+  if (A.prof) {
+    for (int d = 32; d >= 1; d >>= 1) pr_lrows += __shfl_xor(pr_lrows, d);
+    if (lane == 0) {
+      atomicAdd(A.prof + 0, pr_rows);
+      atomicAdd(A.prof + 1, pr_cols);
+      atomicAdd(A.prof + 2, pr_lrows);
+      atomicAdd(A.prof + 3, wc);
+    }
+  }
+}
+
 // band adjustment of bandedSWA.cpp:161-170, in the reference's double arithmetic
 static int adjust_w(int w, int qlen, int mx, const gb_bsw_params &p) {
   int max_ins = (int)((double)(qlen * mx + p.end_bonus - p.o_ins) / p.e_ins + 1.);
@@ -252,6 +479,12 @@ static int adjust_w(int w, int qlen, int mx, const gb_bsw_params &p) {
 
 struct gb_bsw_batch {
   int device = -1, num_cus = 0;
+  // launch plan: order[seg[v] .. seg[v+1]) are the pairs of variant v (lane kernels NCH = 4, 8, 12,
+  // 16, 20; v = 5: wave-per-pair kernel), each segment sorted by decreasing target length
+  static constexpr int kVariants = 6;
+  int64_t seg[kVariants + 1] = {0};
+  uint32_t *d_order = nullptr;
+  unsigned long long *d_prof = nullptr;  // GB_BSW_PROF=1 per-variant sweep counters (development aid)
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   gb_bsw_params params{};
@@ -289,7 +522,7 @@ int gb_bsw_batch_destroy(gb_bsw_batch *B) {
   if (!B) return GB_OK;
   if (B->device >= 0) (void)hipSetDevice(B->device);
   if (B->stream) (void)hipStreamSynchronize(B->stream);
-  for (void *p : {(void *)B->d_pairs, (void *)B->d_tgt, (void *)B->d_qry, (void *)B->d_out6, (void *)B->d_cells,
+  for (void *p : {(void *)B->d_prof, (void *)B->d_order, (void *)B->d_pairs, (void *)B->d_tgt, (void *)B->d_qry, (void *)B->d_out6, (void *)B->d_cells,
                   (void *)B->d_total})
     (void)hipFree(p);
   for (auto &e : B->ev)
@@ -320,7 +553,45 @@ int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, in
            "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
     P[p] = {s.idr, s.idq, s.len1, s.len2, s.h0, gbbsw::adjust_w(params->w, s.len2, mx, *params)};
   }
+  // variant per pair: the pair-per-lane kernel needs qlen < 8*NCH (NCH <= 20) and scores that fit
+  // the 16-bit eh packing; everything else goes to the wave-per-pair kernel
+  int mn = 0;
+  for (int k = 0; k < 25; ++k) mn = std::min(mn, (int)params->mat[k]);
+  std::vector<uint8_t> var((size_t)n);
+  // sort key: variant, then query length in steps of 4 (similar band ends per wave), then decreasing
+  // target length (similar row counts per wave)
+  constexpr int kQB = 64, kTB = 4096;
+  auto key = [&](int64_t p) -> size_t {
+    const gbbsw::Pair &q = P[p];
+    return ((size_t)var[p] * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
+           (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1));
+  };
+  const bool lane_ok = params->o_del >= 0 && params->o_ins >= 0 && mn >= -128 && mx <= 127;
+  for (int64_t p = 0; p < n; ++p) {
+    const gbbsw::Pair &q = P[p];
+    int v = 5;
+    if (lane_ok && q.h0 >= 0 && (int64_t)q.h0 + (int64_t)q.qlen * mx < 30000) {
+      const int nch = (q.qlen + 8) / 8;  // columns 0..qlen
+      v = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 12 ? 2 : nch <= 16 ? 3 : nch <= 20 ? 4 : 5;
+    }
+    var[p] = (uint8_t)v;
+  }
+  std::vector<uint32_t> order((size_t)n);
+  {
+    std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * kQB * kTB + 1, 0);
+    for (int64_t p = 0; p < n; ++p) cnt[key(p)]++;
+    int64_t acc = 0;
+    for (auto &c : cnt) {
+      const int64_t t = c;
+      c = acc;
+      acc += t;
+    }
+    for (int64_t p = 0; p < n; ++p) order[cnt[key(p)]++] = (uint32_t)p;
+  }
   auto *B = new gb_bsw_batch();
+  for (int v = 0; v <= gb_bsw_batch::kVariants; ++v) B->seg[v] = 0;
+  for (int64_t p = 0; p < n; ++p) B->seg[var[p] + 1]++;
+  for (int v = 0; v < gb_bsw_batch::kVariants; ++v) B->seg[v + 1] += B->seg[v];
   B->params = *params;
   B->n = n;
   hipError_t e = hipGetDevice(&B->device);
@@ -330,6 +601,8 @@ int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, in
     if (e == hipSuccess) e = hipEventCreate(&ev);
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
   if (e == hipSuccess) e = hipMalloc(&B->d_pairs, nn * sizeof(gbbsw::Pair));
+  if (e == hipSuccess) e = hipMalloc(&B->d_order, nn * sizeof(uint32_t));
+  if (e == hipSuccess && n) e = hipMemcpy(B->d_order, order.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&B->d_tgt, (size_t)std::max<int64_t>(ref_bytes, 1));
   if (e == hipSuccess) e = hipMalloc(&B->d_qry, (size_t)std::max<int64_t>(qer_bytes, 1));
   if (e == hipSuccess) e = hipMalloc(&B->d_out6, nn * 6 * sizeof(int32_t));
@@ -353,31 +626,83 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
   GB_HIP(hipMemsetAsync(B->d_total, 0, 2 * sizeof(unsigned long long), B->stream));
   GB_HIP(hipEventRecord(B->ev[0], B->stream));
   if (B->n > 0) {
-    gbbsw::Args A;
-    A.pairs = B->d_pairs;
-    A.n = B->n;
-    A.tgt = B->d_tgt;
-    A.qry = B->d_qry;
-    A.out6 = B->d_out6;
-    A.cells = B->d_cells;
-    A.total_cells = B->d_total;
-    A.next = reinterpret_cast<unsigned int *>(B->d_total + 1);
-    A.o_del = B->params.o_del;
-    A.e_del = B->params.e_del;
-    A.o_ins = B->params.o_ins;
-    A.e_ins = B->params.e_ins;
-    A.zdrop = B->params.zdrop;
-    std::memset(A.mat, 0, sizeof(A.mat));
-    std::memcpy(A.mat, B->params.mat, 25);
-    const int64_t waves = B->n;
-    const int64_t cap = (int64_t)B->num_cus * gbbsw::kBlocksPerCU;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cap, (waves + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
-    hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0,
-                       B->stream, A);
-    GB_HIP(hipGetLastError());
+    gbbsw::LaneArgs L;
+    L.pairs = B->d_pairs;
+    L.order = B->d_order;
+    L.tgt = B->d_tgt;
+    L.qry = B->d_qry;
+    L.out6 = B->d_out6;
+    L.cells = B->d_cells;
+    L.total_cells = B->d_total;
+    L.o_del = B->params.o_del;
+    L.e_del = B->params.e_del;
+    L.o_ins = B->params.o_ins;
+    L.e_ins = B->params.e_ins;
+    L.zdrop = B->params.zdrop;
+    for (int t = 0; t < 5; ++t) {  // biased score bytes of row t for query codes 0..3 and 4
+      uint32_t lo = 0;
+      for (int q = 0; q < 4; ++q) lo |= (uint32_t)(uint8_t)(B->params.mat[t * 5 + q] + gbbsw::kBias) << (8 * q);
+      L.tab[2 * t] = lo;
+      L.tab[2 * t + 1] = (uint32_t)(uint8_t)(B->params.mat[t * 5 + 4] + gbbsw::kBias) | 0x80808000u;
+    }
+    void (*lane_kernels[5])(gbbsw::LaneArgs) = {gbbsw::bsw_lane_kernel<4>, gbbsw::bsw_lane_kernel<8>,
+                                                 gbbsw::bsw_lane_kernel<12>, gbbsw::bsw_lane_kernel<16>,
+                                                 gbbsw::bsw_lane_kernel<20>};
+    L.prof = nullptr;
+    const char *pe = getenv("GB_BSW_PROF");
+    const bool prof = pe && *pe == '1';
+    if (prof) {
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 20 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 20 * sizeof(unsigned long long), B->stream));
+    }
+    for (int v = 0; v < 5; ++v) {
+      if (prof) L.prof = B->d_prof + 4 * v;
+      L.first = B->seg[v];
+      L.count = B->seg[v + 1] - B->seg[v];
+      if (L.count == 0) continue;
+      hipLaunchKernelGGL(lane_kernels[v], dim3((unsigned)((L.count + 63) / 64)), dim3(64), 0, B->stream, L);
+      GB_HIP(hipGetLastError());
+    }
+    const int64_t nw = B->seg[6] - B->seg[5];
+    if (nw > 0) {
+      gbbsw::Args A;
+      A.pairs = B->d_pairs;
+      A.list = B->d_order + B->seg[5];
+      A.n = nw;
+      A.tgt = B->d_tgt;
+      A.qry = B->d_qry;
+      A.out6 = B->d_out6;
+      A.cells = B->d_cells;
+      A.total_cells = B->d_total;
+      A.next = reinterpret_cast<unsigned int *>(B->d_total + 1);
+      A.o_del = B->params.o_del;
+      A.e_del = B->params.e_del;
+      A.o_ins = B->params.o_ins;
+      A.e_ins = B->params.e_ins;
+      A.zdrop = B->params.zdrop;
+      std::memset(A.mat, 0, sizeof(A.mat));
+      std::memcpy(A.mat, B->params.mat, 25);
+      const int64_t cap = (int64_t)B->num_cus * gbbsw::kBlocksPerCU;
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cap, (nw + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
+      hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0,
+                         B->stream, A);
+      GB_HIP(hipGetLastError());
+    }
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   B->ran = true;
+  if (B->d_prof && getenv("GB_BSW_PROF")) {
+    unsigned long long h[20];
+    GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
+    GB_HIP(hipStreamSynchronize(B->stream));
+    for (int v = 0; v < 5; ++v)
+      if (h[4 * v])
+        fprintf(stderr,
+                "[bsw prof] NCH=%d pairs %lld: wave rows %llu, lane-row use %.3f, column use %.3f (cells %llu / "
+                "lane-column slots %llu)\n",
+                4 * (v + 1), (long long)(B->seg[v + 1] - B->seg[v]), h[4 * v], h[4 * v + 2] / (64.0 * h[4 * v]),
+                h[4 * v + 3] / (64.0 * h[4 * v + 1]), h[4 * v + 3], 64 * h[4 * v + 1]);
+  }
   return GB_OK;
 }
 

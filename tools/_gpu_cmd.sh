@@ -1,4 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu -k "cli" > gpurun_out/pytest_cli.log 2>&1; st=$?; tail -30 gpurun_out/pytest_cli.log; exit $st
+timeout -k 10 600 python -m pytest tests/test_bsw.py -x -q -m gpu 2>&1 | tail -2
+GB_BSW_PROF=1 timeout -k 10 300 python tools/bsw_probe.py 2>&1 | grep -v amdgpu.ids | tail -7
