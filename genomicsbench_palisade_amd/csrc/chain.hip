@@ -169,36 +169,28 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
         scj = 0;
         pj = -1;
       }
-      // ---- candidate score (host_kernel.cpp:55-82), lane-parallel ---------------------------
-      bool ok = valid;
-      int32_t sc = INT_MIN;
-      if (ok) {
-        const int64_t dr = (int64_t)(xi - xj);
-        const int32_t dq = qi - (int32_t)yj;
-        const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
-        if ((sidi == sidj && dr == 0) || dq <= 0) ok = false;
-        if ((sidi == sidj && dq > max_dist_y) || dq > max_dist_x) ok = false;
-        const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
-        if (sidi == sidj && dd > bw) ok = false;
-        if (n_segs > 1 && sidi == sidj && dr > max_dist_y) ok = false;  // is_cdna = 0
-        if (ok) {
-          const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
-          int32_t s = (int32_t)(min_d > q_span ? (int64_t)q_span : (dq < dr ? (int64_t)dq : dr));
-          const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
-          int gap_cost = 0;
-          if (sidi != sidj) {
-            const int c_lin = (int)((double)dd * .01 * avg_qspan), c_log = log_dd;
-            if (dr == 0)
-              ++s;
-            else
-              gap_cost = c_lin < c_log ? c_lin : c_log;
-          } else {
-            gap_cost = (int)((double)dd * .01 * avg_qspan) + (log_dd >> 1);
-          }
-          s -= (int)((double)gap_cost * (double)1.0f + .499);
-          sc = s + scj;
-        }
+      // ---- candidate score (host_kernel.cpp:55-82), lane-parallel and branch-free -------------
+      const int64_t dr = (int64_t)(xi - xj);
+      const int32_t dq = qi - (int32_t)yj;
+      const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
+      const bool same = sidi == sidj;
+      const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
+      const bool ok = valid && !((same && dr == 0) || dq <= 0) && !((same && dq > max_dist_y) || dq > max_dist_x) &&
+                      !(same && dd > bw) && !(n_segs > 1 && same && dr > max_dist_y);  // is_cdna = 0
+      const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
+      const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
+      const int c_lin = (int)((double)dd * .01 * avg_qspan);
+      int32_t s0 = min_d > q_span ? q_span : min_d;
+      int gap_cost;
+      if (!same) {
+        s0 += dr == 0 ? 1 : 0;
+        gap_cost = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
+      } else {
+        gap_cost = c_lin + (log_dd >> 1);
       }
+      // (int)((double)gap_cost * gap_scale + .499) with gap_scale == 1.0f (host_kernel.cpp:36) is
+      // gap_cost itself for 0 <= gap_cost < 2^31
+      const int32_t sc = ok ? s0 - gap_cost + scj : INT_MIN;
       // ---- "targets[j] == i": stamps from visited j' > j with parents[j'] == j --------------
       if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
       const bool tgt = valid && S[j & (kRing - 1)] == stamp;

@@ -36,9 +36,37 @@ constexpr int kCap = 40;       // first-pass SMEM slots per read (~8 on average 
 constexpr int kBigCap = 2048;  // second pass, for the rare reads that overflow the first
 constexpr int kMaxOvf = 16384; // reads the second pass can take
 
-struct __attribute__((aligned(16))) Ent {  // one `prev` entry (SMEM without rid)
+struct Ent {  // one `prev` entry (SMEM without rid), unpacked in registers
   int64_t k, l, s;
   uint32_t m, n;
+};
+
+// In memory an entry is 16 bytes: k, l, s < 2^34 rows and m, n < 2^13 read positions (checked on
+// the host), laid out wave-interleaved (entry e of lane t of wave w at [(w * stride + e) * 64 + t])
+// so the lanes of a wave touching the same list depth hit the same lines.
+struct __attribute__((aligned(16))) PEnt {
+  uint64_t w0, w1;
+};
+__device__ __forceinline__ PEnt pack_ent(const Ent &e) {
+  PEnt p;
+  p.w0 = (uint64_t)e.k | ((uint64_t)e.l << 34);
+  p.w1 = ((uint64_t)e.l >> 30) | ((uint64_t)e.s << 4) | ((uint64_t)e.m << 38) | ((uint64_t)e.n << 51);
+  return p;
+}
+__device__ __forceinline__ Ent unpack_ent(const PEnt &p) {
+  constexpr uint64_t M34 = (1ull << 34) - 1, M13 = (1ull << 13) - 1;
+  Ent e;
+  e.k = (int64_t)(p.w0 & M34);
+  e.l = (int64_t)((p.w0 >> 34) | ((p.w1 & 0xFull) << 30));
+  e.s = (int64_t)((p.w1 >> 4) & M34);
+  e.m = (uint32_t)((p.w1 >> 38) & M13);
+  e.n = (uint32_t)((p.w1 >> 51) & M13);
+  return e;
+}
+struct PList {  // one lane's view of its wave-interleaved scratch
+  PEnt *base;   // &scratch[(wave * stride) * 64 + lane]
+  __device__ __forceinline__ Ent get(int e) const { return unpack_ent(base[(size_t)e * 64]); }
+  __device__ __forceinline__ void put(int e, const Ent &v) const { base[(size_t)e * 64] = pack_ent(v); }
 };
 
 struct DevIndex {
@@ -100,15 +128,16 @@ struct SearchArgs {
   const uint8_t *qdb;
   const int32_t *lens;
   int32_t nreads, stride, min_seed_len, split_len;
-  Ent *scratch;          // per lane: stride entries
-  gb_smem *slots;        // per slot: cap entries (pass 1: slot = read, pass 2: list position)
+  PEnt *scratch;         // per wave: stride x 64 entries, wave-interleaved
+  gb_smem *slots;        // per read: cap entries
+  gb_smem *big;          // kMaxOvf promoted slots of kBigCap entries
   int32_t cap;
   const int32_t *list;   // pass 2: reads to redo (null in pass 1)
   const int32_t *list_n; // pass 2: number of reads in `list`
   int32_t *counts;       // per read: total SMEMs
   int32_t *phase;        // per read: num_smem1, num_smem2, num_smem3
   int32_t *next_read;    // work counter
-  int32_t *ovf_list;     // pass 1: reads that exceeded cap (redone by pass 2)
+  int32_t *ovf_list;     // promoted reads, by big-slot index
   int32_t *ovf_n;
   int32_t *fatal;        // pass 2 overflow / list overflow
   unsigned long long *bwt_calls;
@@ -118,10 +147,33 @@ __device__ __forceinline__ bool smem_less(const gb_smem &a, const gb_smem &b) {
   return a.m < b.m || (a.m == b.m && a.n > b.n);  // compare_smem, FMI_search.cpp:1499-1518
 }
 
+__device__ void heap_sort(gb_smem *a, int n) {
+  auto sift = [&](int root, int end) {
+    while (true) {
+      int child = 2 * root + 1;
+      if (child >= end) return;
+      if (child + 1 < end && smem_less(a[child], a[child + 1])) child++;
+      if (!smem_less(a[root], a[child])) return;
+      const gb_smem t = a[root];
+      a[root] = a[child];
+      a[child] = t;
+      root = child;
+    }
+  };
+  for (int start = n / 2 - 1; start >= 0; start--) sift(start, n);
+  for (int end = n - 1; end > 0; end--) {
+    const gb_smem t = a[0];
+    a[0] = a[end];
+    a[end] = t;
+    sift(0, end);
+  }
+}
+
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
-  Ent *const prev = A.scratch + (size_t)gid * A.stride;
+  PList prev;
+  prev.base = A.scratch + (size_t)(gid >> 6) * A.stride * 64 + (gid & 63);
   unsigned long long calls = 0, calls_read = 0;  // backwardExt calls (all reads / this read)
 
   int st = NEXT_READ;
@@ -134,10 +186,23 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   bool first = true;
   int64_t ck = 0, cl = 0, cs = 0;  // current SMEM of a forward extension
   uint32_t cm = 0;
-  Ent *r = prev;                   // reversed prev list: r[0] = last pushed
+  int r0 = 0;                      // reversed prev list: r[p] = prev[r0 + p] (r[0] = last pushed)
+  Ent cur{};                       // the prev entry of the pending BWD_P request
 
+  int cap = A.cap;  // slots of the current output area (kCap, or kBigCap once promoted)
   auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
-    if (nout < A.cap) {
+    if (nout == cap && cap == kCap) {
+      // promote the read to a big slot (first pass only, rare): copy what it has and carry on there
+      const int kb = atomicAdd(A.ovf_n, 1);
+      if (kb < kMaxOvf) {
+        gb_smem *big = A.big + (size_t)kb * kBigCap;
+        for (int t = 0; t < kCap; t++) big[t] = o[t];
+        o = big;
+        cap = kBigCap;
+        A.ovf_list[kb] = rd;
+      }
+    }
+    if (nout < cap) {
       gb_smem e;
       e.rid = (uint32_t)rd;
       e.m = m;
@@ -169,6 +234,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
           o = A.slots + (size_t)slot * A.cap;
+          cap = A.cap;
           nout = 0;
           ovf = false;
           calls_read = 0;
@@ -222,10 +288,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           if (cs >= min_intv) {
             Ent e;
             e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);  // current n = j-1
-            prev[L - 1 - numPrev] = e;
+            prev.put(L - 1 - numPrev, e);
             numPrev++;
           }
-          r = prev + (L - numPrev);
+          r0 = L - numPrev;
           j = x - 1;
           st = BWD_ITER;
           break;
@@ -256,18 +322,16 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             }
             break;
           }
-          {
-            const Ent e = r[p];
-            rk = e.k;
-            rl = e.l;
-            rs = e.s;
-            rb = a;
-            req = true;
-          }
+          cur = prev.get(r0 + p);
+          rk = cur.k;
+          rl = cur.l;
+          rs = cur.s;
+          rb = a;
+          req = true;
           break;
         case BWD_FINAL:
           if (numPrev != 0) {
-            const Ent e = r[0];
+            const Ent e = prev.get(r0);
             if ((e.n - e.m + 1) >= (uint32_t)A.min_seed_len) emit(e.k, e.l, e.s, e.m, e.n);
           }
           st = OP_END;
@@ -285,7 +349,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           // fmi.cpp:293-302: SMEMs of length >= split_len with s <= splitWidth(10) restart at
           // the midpoint with min_intv = s + 1
           bool found = false;
-          while (ridx < n1 && ridx < A.cap) {
+          while (ridx < n1 && ridx < cap) {
             const gb_smem e = o[ridx];
             const int start = (int)e.m, end = (int)e.n + 1;
             if (!(end - start < A.split_len || e.s > 10)) {
@@ -344,33 +408,26 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           req = true;
           break;
         case FINISH: {
-          const int n = nout < A.cap ? nout : A.cap;
-          for (int i = 1; i < n; i++) {  // insertion sort by (m asc, n desc)
-            const gb_smem e = o[i];
-            int t = i - 1;
-            while (t >= 0 && smem_less(e, o[t])) {
-              o[t + 1] = o[t];
-              t--;
+          const int n = nout < cap ? nout : cap;
+          if (n <= 48) {
+            for (int i = 1; i < n; i++) {  // insertion sort by (m asc, n desc)
+              const gb_smem e = o[i];
+              int t = i - 1;
+              while (t >= 0 && smem_less(e, o[t])) {
+                o[t + 1] = o[t];
+                t--;
+              }
+              o[t + 1] = e;
             }
-            o[t + 1] = e;
+          } else {
+            heap_sort(o, n);  // promoted reads: O(n log n) (equal keys are identical SMEMs)
           }
           A.counts[rd] = nout;
           A.phase[3 * rd + 0] = n1;
           A.phase[3 * rd + 1] = n2;
           A.phase[3 * rd + 2] = nout - n1 - n2;
-          // a read redone by pass 2 is counted there, not here
-          if (!ovf || A.list) calls += calls_read;
-          if (ovf) {
-            if (A.list) {
-              atomicAdd(A.fatal, 1);
-            } else {
-              const int k = atomicAdd(A.ovf_n, 1);
-              if (k < kMaxOvf)
-                A.ovf_list[k] = rd;
-              else
-                atomicAdd(A.fatal, 1);
-            }
-          }
+          calls += calls_read;
+          if (ovf) atomicAdd(A.fatal, 1);  // more than kBigCap SMEMs, or the big-slot pool was exhausted
           st = NEXT_READ;
           break;
         }
@@ -393,7 +450,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       if (ns != cs) {  // push the current SMEM (prevArray[numPrev] = smem; numPrev += s_neq)
         Ent e;
         e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);
-        prev[L - 1 - numPrev] = e;
+        prev.put(L - 1 - numPrev, e);
         numPrev++;
       }
       if (ns < min_intv) {
@@ -406,7 +463,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         j++;
       }
     } else if (st == BWD_P) {
-      const Ent e = r[p];
+      const Ent e = cur;
       if (first) {
         if (so < min_intv && (e.n - e.m + 1) >= (uint32_t)A.min_seed_len) {
           emit(e.k, e.l, e.s, e.m, e.n);
@@ -415,14 +472,14 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           curr_s = (int)so;
           Ent ne;
           ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
-          r[numCurr++] = ne;
+          prev.put(r0 + numCurr++, ne);
           first = false;
         }
       } else if (so >= min_intv && so != (int64_t)curr_s) {
         curr_s = (int)so;
         Ent ne;
         ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
-        r[numCurr++] = ne;
+        prev.put(r0 + numCurr++, ne);
       }
       p++;
     } else {  // P3_NEXT (bwtSeedStrategyAllPosOneThread)
@@ -475,7 +532,7 @@ struct gb_fmi_reads {
   int lanes = 0;
   uint8_t *d_qdb = nullptr;
   int32_t *d_lens = nullptr;
-  gbfmi::Ent *d_scratch = nullptr;
+  gbfmi::PEnt *d_scratch = nullptr;
   gb_smem *d_slots = nullptr;
   int32_t *d_counts = nullptr;
   int32_t *d_phase = nullptr;
@@ -583,8 +640,9 @@ int gb_fmi_index_destroy(gb_fmi_index *idx) {
 int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens,
                         int32_t num_reads, int32_t max_readlength, gb_fmi_reads **out) {
   GB_ARG(idx && out && (num_reads == 0 || (enc_qdb && lens)), "gb_fmi_reads_create: null argument");
-  GB_ARG(num_reads >= 0 && max_readlength > 0 && max_readlength < 10000,
-         "gb_fmi_reads_create: bad sizes (reads %d, max_readlength %d)", num_reads, max_readlength);
+  GB_ARG(num_reads >= 0 && max_readlength > 0 && max_readlength < 8192,
+         "gb_fmi_reads_create: bad sizes (reads %d, max_readlength %d; need < 8192)", num_reads, max_readlength);
+  GB_ARG(idx && idx->n < (1ll << 34), "gb_fmi_reads_create: index too large for 34-bit list entries");
   for (int32_t r = 0; r < num_reads; r++)
     GB_ARG(lens[r] >= 0 && lens[r] <= max_readlength, "read %d: length %d > max_readlength %d", r,
            lens[r], max_readlength);
@@ -600,7 +658,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     if (e == hipSuccess) e = hipEventCreate(&ev);
   if (e == hipSuccess) e = hipMalloc(&R->d_qdb, nr * (size_t)max_readlength);
   if (e == hipSuccess) e = hipMalloc(&R->d_lens, nr * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::Ent));
+  if (e == hipSuccess) e = hipMalloc(&R->d_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::PEnt));
   if (e == hipSuccess) e = hipMalloc(&R->d_slots, nr * gbfmi::kCap * sizeof(gb_smem));
   if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&R->d_ovf_pos, nr * sizeof(int32_t));
@@ -666,23 +724,15 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   A.fatal = R->d_ctl + 2;
   A.bwt_calls = R->d_calls;
   if (R->nreads > 0) {
-    // pass 1: every read, kCap slots each
+    // one pass: every read, kCap slots each; a read that outgrows them is promoted in place to a
+    // kBigCap slot of the d_big pool
     A.slots = R->d_slots;
+    A.big = R->d_big;
     A.cap = gbfmi::kCap;
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
     hipLaunchKernelGGL(gbfmi::smem_search, dim3(blocks), dim3(64), 0, R->stream, A);
-    GB_HIP(hipGetLastError());
-    // pass 2: the reads that overflowed (usually none), kBigCap slots each; the read count stays
-    // on the device, idle lanes exit at once
-    A.slots = R->d_big;
-    A.cap = gbfmi::kBigCap;
-    A.list = R->d_ovf_list;
-    A.list_n = R->d_ctl + 1;
-    A.next_read = R->d_ctl + 3;
-    A.bwt_calls = R->d_calls;
-    hipLaunchKernelGGL(gbfmi::smem_search, dim3(32), dim3(64), 0, R->stream, A);
     GB_HIP(hipGetLastError());
     hipLaunchKernelGGL(gbfmi::mark_overflow, dim3((gbfmi::kMaxOvf + 255) / 256), dim3(256), 0, R->stream,
                        R->d_ovf_list, R->d_ctl + 1, R->d_ovf_pos);
