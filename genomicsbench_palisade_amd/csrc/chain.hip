@@ -97,10 +97,89 @@ __device__ __forceinline__ int32_t load_l2(const int32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1 (bypasses L1)
 }
 
-__global__ __launch_bounds__(64) void chain_kernel(Args A) {
+// Pair geometry of anchor i against candidate j (host_kernel.cpp:55-82 without score[j]): whether j
+// passes the filters, and s = min(q_span, dq, dr) (+1 paired bonus) - gap_cost.
+__device__ __forceinline__ bool geometry(uint64_t xi, uint64_t yi, uint64_t xj, uint64_t yj, bool valid,
+                                         int max_dist_x, int max_dist_y, int bw, int n_segs, double avg_qspan,
+                                         int32_t &sg) {
+  const int32_t qi = (int32_t)yi, q_span = (int32_t)(yi >> 32 & 0xff);
+  const int32_t sidi = (int32_t)((yi & (0xffull << 48)) >> 48);
+  const int64_t dr = (int64_t)(xi - xj);
+  const int32_t dq = qi - (int32_t)yj;
+  const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
+  const bool same = sidi == sidj;
+  const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
+  const bool ok = valid && !((same && dr == 0) || dq <= 0) && !((same && dq > max_dist_y) || dq > max_dist_x) &&
+                  !(same && dd > bw) && !(n_segs > 1 && same && dr > max_dist_y);  // is_cdna = 0
+  const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
+  const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
+  const int c_lin = (int)((double)dd * .01 * avg_qspan);
+  int32_t s0 = min_d > q_span ? q_span : min_d;
+  int gap_cost;
+  if (!same) {
+    s0 += dr == 0 ? 1 : 0;
+    gap_cost = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
+  } else {
+    gap_cost = c_lin + (log_dd >> 1);
+  }
+  // (int)((double)gap_cost * gap_scale + .499) with gap_scale == 1.0f (host_kernel.cpp:36) is
+  // gap_cost itself for 0 <= gap_cost < 2^31
+  sg = s0 - gap_cost;
+  return ok;
+}
+
+// One 64-candidate step in visiting order (lane l = j = jtop - l): running max_f, n_skip, the
+// break and the targets/stamps. Updates M, J, N; returns the break lane (64 = none).
+__device__ __forceinline__ int resolve_step(int32_t sc, bool ok, bool valid, int32_t pj, int64_t j, int64_t jtop,
+                                            int64_t st, uint32_t stamp, int lane, int32_t *__restrict__ target,
+                                            int64_t i, uint32_t *S, int32_t &M, int64_t &J, int32_t &N,
+                                            unsigned long long &vis) {
+  // "targets[j] == i": stamps from visited j' > j with parents[j'] == j
+  if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
+  const bool tgt = valid && S[j & (kRing - 1)] == stamp;
+  const int32_t mx = scan_max(ok ? sc : INT_MIN);  // inclusive max scan
+  const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
+  const bool upd = ok && sc > before;
+  int32_t a = upd ? -1 : ((ok && tgt) ? 1 : 0), b = 0;  // n -> max(n + a, b); n >= 0 always
+  scan_compose(a, b);
+  const int32_t n_after = max(N + a, b);
+  const bool brk = ok && !upd && tgt && n_after > kMaxSkip;
+  const uint64_t bm = __ballot(brk);
+  const int bl = bm ? __builtin_ctzll(bm) : 64;
+  const int64_t nvalid = min((int64_t)64, jtop - st + 1);
+  vis += (bl < 64) ? (unsigned long long)(bl + 1) : (unsigned long long)nvalid;
+  const uint64_t low = bl >= 64 ? ~0ull : ((1ull << bl) - 1);
+  const uint64_t um = __ballot(upd) & low;
+  if (um) {
+    const int lu = 63 - __builtin_clzll(um);
+    J = jtop - lu;
+    M = __builtin_amdgcn_readlane(mx, lu);
+  }
+  if (ok && lane < bl && pj >= 0) target[pj] = (int32_t)i;
+  N = __builtin_amdgcn_readlane(n_after, 63);
+  return bl;
+}
+
+// Producer -> consumer hand-off, one slot per anchor i: the geometry of its first 64 candidates.
+constexpr int kSlots = 16;
+struct Slot {
+  int32_t sg[64];
+  uint64_t okmask;
+  int64_t st;
+  uint64_t xi, yi;
+};
+
+// Two waves per call. The anchors' pair geometry (filters, gap costs; no scores involved) runs ahead
+// in the producer wave and is handed over through an LDS ring; the consumer wave keeps only the
+// score-dependent sequential part (max_f / n_skip scans, break, targets, outputs), so the critical
+// path of a long call is roughly halved. Hand-off words are LDS counters polled with s_sleep.
+__global__ __launch_bounds__(128) void chain_kernel(Args A) {
   __shared__ uint32_t S[kRing];
+  __shared__ Slot ring[kSlots];
+  __shared__ int produced, consumed;
   const int c = A.order[blockIdx.x];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool producer = threadIdx.x >= 64;
   const int64_t o = A.offsets[c];
   const int64_t n = A.offsets[c + 1] - o;
   const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
@@ -110,36 +189,65 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
   const const_u64 *XC = (const const_u64 *)X, *YC = (const const_u64 *)Y;
   int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
 
-  for (int k = lane; k < kRing; k += 64) S[k] = 0;
-  for (int64_t k = lane; k < n; k += 64) target[k] = 0;  // a fresh std::vector in the reference
+  for (int k = threadIdx.x; k < kRing; k += 128) S[k] = 0;
+  for (int64_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
+  if (threadIdx.x == 0) produced = consumed = 0;
   __builtin_amdgcn_s_waitcnt(0);  // zeroing stores complete before any later targets store
   __syncthreads();
 
-  // register window: lane l holds anchor i-1-l
-  uint64_t wx = 0, wy = 0;
-  int32_t ws = 0, wpar = -1, wpk = 0;
-  uint64_t px = 0, py = 0;  // anchor i-1
-  int32_t ps = 0, pp = -1, pk = 0;
-  int64_t st = 0;
+  if (producer) {
+    // ---------------- producer: geometry of anchor i against i-1-lane --------------------------
+    uint64_t wx = 0, wy = 0;  // lane l: anchor i-1-l
+    int64_t st = 0;
+    for (int64_t i = 0; i < n; i++) {
+      const uint64_t xi = XC[i], yi = YC[i];
+      while (st < i && xi > XC[st] + (uint64_t)(int64_t)max_dist_x) ++st;
+      if (i - st > kMaxIter) st = i - kMaxIter;
+      int32_t sg;
+      const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+      const uint64_t okm = __ballot(ok);
+      // wait for a free slot
+      while (i - (int64_t)__hip_atomic_load(&consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= kSlots)
+        __builtin_amdgcn_s_sleep(1);
+      Slot &sl = ring[i & (kSlots - 1)];
+      sl.sg[lane] = sg;
+      if (lane == 0) {
+        sl.okmask = okm;
+        sl.st = st;
+        sl.xi = xi;
+        sl.yi = yi;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // slot contents land before the count that publishes them
+      if (lane == 0) __hip_atomic_store(&produced, (int)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      wx = dpp_shr_u64(wx, xi);
+      wy = dpp_shr_u64(wy, yi);
+    }
+    return;
+  }
+
+  // ---------------- consumer ---------------------------------------------------------------------
+  int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l
   unsigned long long vis = 0;
   unsigned long long c_head = 0, c_step = 0, c_tail = 0, n_step = 0, t_0 = 0, t_1 = 0;
   const bool prof = A.prof != nullptr;
   for (int64_t i = 0; i < n; i++) {
     if (prof) t_0 = __builtin_amdgcn_s_memtime();
-    if (i > 0) {
-      wx = dpp_shr_u64(wx, px);
-      wy = dpp_shr_u64(wy, py);
-      ws = dpp_shr_i32(ws, ps);
-      wpar = dpp_shr_i32(wpar, pp);
-      wpk = dpp_shr_i32(wpk, pk);
+    if ((i & 63) == 0 && i > 0) {  // flush the window: anchors i-64 .. i-1 (lane l: i-1-l)
+      score[i - 1 - lane] = ws;
+      parent[i - 1 - lane] = wpar;
+      peak[i - 1 - lane] = wpk;
+      __builtin_amdgcn_s_waitcnt(0);  // flushed anchors are in L2 before any older-candidate read
     }
-    if ((i & 31) == 0) __builtin_amdgcn_s_waitcnt(0);  // stores of steps <= i-32 are in L2
-    const uint64_t xi = XC[i], yi = YC[i];  // scalar loads
-    const int32_t qi = (int32_t)yi, q_span = (int32_t)(yi >> 32 & 0xff);
-    const int32_t sidi = (int32_t)((yi & (0xffull << 48)) >> 48);
-    while (st < i && xi > XC[st] + (uint64_t)(int64_t)max_dist_x) ++st;
-    if (i - st > kMaxIter) st = i - kMaxIter;
-
+    while ((int64_t)__hip_atomic_load(&produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= i)
+      __builtin_amdgcn_s_sleep(1);
+    const Slot &sl = ring[i & (kSlots - 1)];
+    const int32_t sg = sl.sg[lane];
+    const bool ok = (sl.okmask >> lane) & 1;
+    const int64_t st = sl.st;
+    const uint64_t xi = sl.xi, yi = sl.yi;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0) __hip_atomic_store(&consumed, (int)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int32_t q_span = (int32_t)(yi >> 32 & 0xff);
     int32_t M = q_span, N = 0;
     int64_t J = -1;
     const uint32_t stamp = (uint32_t)(i + 1);
@@ -148,75 +256,32 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
       c_head += t_1 - t_0;
       t_0 = t_1;
     }
-    for (int64_t jtop = i - 1; jtop >= st; jtop -= 64) {
+    const int64_t jtop = i - 1;
+    int bl = 64;
+    if (jtop >= st) {
       if (prof) ++n_step;
       const int64_t j = jtop - lane;
-      const bool valid = j >= st;
-      uint64_t xj, yj;
-      int32_t scj, pj;
-      if (jtop == i - 1) {
-        xj = wx;
-        yj = wy;
-        scj = ws;
-        pj = wpar;
-      } else if (valid) {
-        xj = X[j];
-        yj = Y[j];
-        scj = load_l2(score + j);
-        pj = load_l2(parent + j);
-      } else {
-        xj = yj = 0;
-        scj = 0;
-        pj = -1;
+      bl = resolve_step(ok ? sg + ws : INT_MIN, ok, j >= st, wpar, j, jtop, st, stamp, lane, target, i, S, M, J, N, vis);
+    }
+    if (bl == 64 && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
+      for (int64_t jt = jtop - 64; jt >= st; jt -= 64) {
+        if (prof) ++n_step;
+        const int64_t jj = jt - lane;
+        const bool v = jj >= st;
+        uint64_t xj = 0, yj = 0;
+        int32_t scj = 0, pj = -1;
+        if (v) {
+          xj = X[jj];
+          yj = Y[jj];
+          scj = load_l2(score + jj);
+          pj = load_l2(parent + jj);
+        }
+        int32_t sgo;
+        const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
+        if (resolve_step(oko ? sgo + scj : INT_MIN, oko, v, pj, jj, jt, st, stamp, lane, target, i, S, M, J, N,
+                         vis) < 64)
+          break;
       }
-      // ---- candidate score (host_kernel.cpp:55-82), lane-parallel and branch-free -------------
-      const int64_t dr = (int64_t)(xi - xj);
-      const int32_t dq = qi - (int32_t)yj;
-      const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
-      const bool same = sidi == sidj;
-      const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
-      const bool ok = valid && !((same && dr == 0) || dq <= 0) && !((same && dq > max_dist_y) || dq > max_dist_x) &&
-                      !(same && dd > bw) && !(n_segs > 1 && same && dr > max_dist_y);  // is_cdna = 0
-      const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
-      const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
-      const int c_lin = (int)((double)dd * .01 * avg_qspan);
-      int32_t s0 = min_d > q_span ? q_span : min_d;
-      int gap_cost;
-      if (!same) {
-        s0 += dr == 0 ? 1 : 0;
-        gap_cost = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
-      } else {
-        gap_cost = c_lin + (log_dd >> 1);
-      }
-      // (int)((double)gap_cost * gap_scale + .499) with gap_scale == 1.0f (host_kernel.cpp:36) is
-      // gap_cost itself for 0 <= gap_cost < 2^31
-      const int32_t sc = ok ? s0 - gap_cost + scj : INT_MIN;
-      // ---- "targets[j] == i": stamps from visited j' > j with parents[j'] == j --------------
-      if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
-      const bool tgt = valid && S[j & (kRing - 1)] == stamp;
-      // ---- sequential order as prefix scans over lanes ---------------------------------------
-      int32_t mx = scan_max(ok ? sc : INT_MIN);  // inclusive max scan
-      const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
-      const bool upd = ok && sc > before;
-      int32_t a = upd ? -1 : ((ok && tgt) ? 1 : 0), b = 0;  // n -> max(n + a, b); n >= 0 always
-      scan_compose(a, b);
-      const int32_t n_after = max(N + a, b);
-      const bool brk = ok && !upd && tgt && n_after > kMaxSkip;
-      const uint64_t bm = __ballot(brk);
-      const int bl = bm ? __builtin_ctzll(bm) : 64;
-      const int64_t nvalid = min((int64_t)64, jtop - st + 1);
-      vis += (bl < 64) ? (unsigned long long)(bl + 1) : (unsigned long long)nvalid;
-      // processed lanes l < bl: max_f, max_j, targets
-      const uint64_t low = bl >= 64 ? ~0ull : ((1ull << bl) - 1);
-      const uint64_t um = __ballot(upd) & low;
-      if (um) {
-        const int lu = 63 - __builtin_clzll(um);
-        J = jtop - lu;
-        M = __builtin_amdgcn_readlane(mx, lu);
-      }
-      if (ok && lane < bl && pj >= 0) target[pj] = (int32_t)i;
-      if (bl < 64) break;
-      N = __builtin_amdgcn_readlane(n_after, 63);
     }
     if (prof) {
       t_1 = __builtin_amdgcn_s_memtime();
@@ -231,17 +296,19 @@ __global__ __launch_bounds__(64) void chain_kernel(Args A) {
         pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
     }
     const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
-    if (lane == 0) {
-      score[i] = M;
-      parent[i] = (int32_t)J;
-      peak[i] = pki;
-    }
+    ws = dpp_shr_i32(ws, M);
+    wpar = dpp_shr_i32(wpar, (int32_t)J);
+    wpk = dpp_shr_i32(wpk, pki);
     if (prof) c_tail += __builtin_amdgcn_s_memtime() - t_0;
-    px = xi;
-    py = yi;
-    ps = M;
-    pp = (int32_t)J;
-    pk = pki;
+  }
+  // final flush: anchors max(0, n - r) .. n-1 with r = n mod 64 (or 64)
+  {
+    const int64_t r = ((n - 1) & 63) + 1;
+    if (lane < r) {
+      score[n - 1 - lane] = ws;
+      parent[n - 1 - lane] = wpar;
+      peak[n - 1 - lane] = wpk;
+    }
   }
   // wave-reduce the visited count
   if (prof && lane == 0) {
@@ -348,7 +415,7 @@ int gb_chain_batch_run(gb_chain_batch *B) {
       GB_HIP(hipMemsetAsync(B->d_prof, 0, 4 * sizeof(unsigned long long), B->stream));
       A.prof = B->d_prof;
     }
-    hipLaunchKernelGGL(gbchain::chain_kernel, dim3((unsigned)B->ncalls), dim3(64), 0, B->stream, A);
+    hipLaunchKernelGGL(gbchain::chain_kernel, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));

@@ -70,32 +70,42 @@ struct PList {  // one lane's view of its wave-interleaved scratch
 };
 
 struct DevIndex {
-  const CpOcc *occ;
+  const Occ2 *occ;
   int64_t count[5];
   int64_t sentinel;
 };
 
 __device__ __forceinline__ uint64_t occ_mask(int y) { return y ? (~0ull << (64 - y)) : 0ull; }
 
-// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). Both CP_OCC lines are
-// loaded whole (64 B each); when sp and ep share a line the second load is skipped.
+// Occ(b, p) for b = A, C, G, T from one Occ2 line (GET_OCC, FMI_search.h:81-89, over the same
+// counts): T = p - A - C - G - [sentinel < p].
+__device__ __forceinline__ void occ4(const Occ2 &L, int64_t p, int64_t sentinel, int64_t o[4]) {
+  const int y = (int)(p & 127);
+  const uint64_t m0 = y >= 64 ? ~0ull : occ_mask(y), m1 = y > 64 ? occ_mask(y - 64) : 0ull;
+  const int64_t cA = (int64_t)(L.cnt[0] & ((1ull << 40) - 1));
+  const int64_t cC = (int64_t)((L.cnt[0] >> 40) | ((L.cnt[1] & 0xFFFFull) << 24));
+  const int64_t cG = (int64_t)(L.cnt[1] >> 16);
+  o[0] = cA + __popcll(L.a[0] & m0) + __popcll(L.a[1] & m1);
+  o[1] = cC + __popcll(L.c[0] & m0) + __popcll(L.c[1] & m1);
+  o[2] = cG + __popcll(L.g[0] & m0) + __popcll(L.g[1] & m1);
+  o[3] = p - o[0] - o[1] - o[2] - (sentinel < p ? 1 : 0);
+}
+
+// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). One 64-byte line covers
+// 128 rows; when sp and ep share a line the second load is skipped.
 __device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l, int64_t s, int a,
                                         int64_t &ko, int64_t &lo, int64_t &so) {
   const int64_t sp = k, ep = k + s;
-  const int64_t bs = sp >> 6, be = ep >> 6;
-  const CpOcc A = F.occ[bs];
-  CpOcc B;
+  const int64_t bs = sp >> 7, be = ep >> 7;
+  const Occ2 A = F.occ[bs];
+  Occ2 B;
   if (be != bs)
     B = F.occ[be];
   else
     B = A;
-  const uint64_t ms = occ_mask((int)(sp & 63)), me = occ_mask((int)(ep & 63));
   int64_t os[4], oe[4];
-#pragma unroll
-  for (int b = 0; b < 4; b++) {
-    os[b] = A.cp_count[b] + __popcll(A.one_hot_bwt_str[b] & ms);
-    oe[b] = B.cp_count[b] + __popcll(B.one_hot_bwt_str[b] & me);
-  }
+  occ4(A, sp, F.sentinel, os);
+  occ4(B, ep, F.sentinel, oe);
   const int64_t off = (k <= F.sentinel && k + s > F.sentinel) ? 1 : 0;
   const int64_t s3 = oe[3] - os[3], s2 = oe[2] - os[2], s1 = oe[1] - os[1], s0 = oe[0] - os[0];
   const int64_t l3 = l + off, l2 = l3 + s3, l1 = l2 + s2, l0 = l1 + s1;
@@ -105,6 +115,41 @@ __device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l,
     case 2: ko = F.count[2] + os[2]; so = s2; lo = l2; break;
     default: ko = F.count[3] + os[3]; so = s3; lo = l3; break;
   }
+}
+
+// byte codes -> 4-bit codes, 8 per word (base b of word w at bits 4*(b))
+__global__ void pack_q4(const uint8_t *__restrict__ qdb, int32_t stride, int32_t nreads, int32_t q4_stride,
+                        uint32_t *__restrict__ q4) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = t / q4_stride, w = t % q4_stride;
+  if (r >= nreads) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 8; b++) {
+    const int64_t j = w * 8 + b;
+    const uint32_t c = j < stride ? min((uint32_t)qdb[r * stride + j], 15u) : 4u;
+    v |= c << (4 * b);
+  }
+  q4[r * q4_stride + w] = v;
+}
+
+// CP_OCC (64 rows per line) -> Occ2 (128 rows per line)
+__global__ void compress_occ(const CpOcc *__restrict__ occ, int64_t cp_size, Occ2 *__restrict__ occ2,
+                             int64_t cp2_size) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cp2_size) return;
+  const CpOcc &b0 = occ[2 * i];
+  const bool has1 = 2 * i + 1 < cp_size;
+  Occ2 L;
+  L.a[0] = b0.one_hot_bwt_str[0];
+  L.c[0] = b0.one_hot_bwt_str[1];
+  L.g[0] = b0.one_hot_bwt_str[2];
+  L.a[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[0] : 0;
+  L.c[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[1] : 0;
+  L.g[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[2] : 0;
+  const uint64_t cA = (uint64_t)b0.cp_count[0], cC = (uint64_t)b0.cp_count[1], cG = (uint64_t)b0.cp_count[2];
+  L.cnt[0] = cA | (cC << 40);
+  L.cnt[1] = (cC >> 24) | (cG << 16);
+  occ2[i] = L;
 }
 
 enum State : int {
@@ -126,6 +171,8 @@ enum State : int {
 struct SearchArgs {
   DevIndex F;
   const uint8_t *qdb;
+  const uint32_t *q4;    // nibble-packed copy of qdb (8 bases per word), q4_stride words per read
+  int32_t q4_stride;
   const int32_t *lens;
   int32_t nreads, stride, min_seed_len, split_len;
   PEnt *scratch;         // per wave: stride x 64 entries, wave-interleaved
@@ -169,7 +216,15 @@ __device__ void heap_sort(gb_smem *a, int n) {
   }
 }
 
+// Reads up to kQBases bases are staged, 4 bits per base, in the lane's LDS row when the lane takes
+// the read (one pass of dword loads from the nibble-packed copy d_q4), so the base lookups of the
+// state machine are LDS reads instead of dependent global byte loads. Longer reads read d_qdb.
+constexpr int kQBases = 160;
+constexpr int kQW = kQBases / 8 + 1;  // words per lane row; odd, so same-word reads are conflict-free
+
+template <bool kLdsQ>
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
+  __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
   PList prev;
@@ -179,6 +234,13 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   int st = NEXT_READ;
   int rd = 0, L = 0, mode = 0;
   const uint8_t *q = nullptr;
+  uint32_t *const qrow = Qs + (kLdsQ ? threadIdx.x * kQW : 0);
+  auto base_at = [&](int idx) -> int {
+    if constexpr (kLdsQ)
+      return (int)((qrow[idx >> 3] >> (4 * (idx & 7))) & 15u);
+    else
+      return q[idx];
+  };
   gb_smem *o = nullptr;
   int nout = 0, n1 = 0, n2 = 0, ridx = 0;
   bool ovf = false;
@@ -233,6 +295,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           rd = A.list ? A.list[slot] : slot;
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
+          if constexpr (kLdsQ) {
+            const uint32_t *src = A.q4 + (size_t)rd * A.q4_stride;
+            for (int w = 0; w < ((L + 7) >> 3); w++) qrow[w] = src[w];
+          }
           o = A.slots + (size_t)slot * A.cap;
           cap = A.cap;
           nout = 0;
@@ -253,7 +319,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             break;
           }
           next_x = x + 1;
-          a = q[x];
+          a = base_at(x);
           if (a >= 4) {
             st = OP_END;
             break;
@@ -272,7 +338,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             break;
           }
           next_x = j + 1;
-          a = q[j];
+          a = base_at(j);
           if (a >= 4) {
             st = FWD_END;
             break;
@@ -300,7 +366,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             st = BWD_FINAL;
             break;
           }
-          a = q[j];
+          a = base_at(j);
           if (a > 3) {
             st = BWD_FINAL;
             break;
@@ -376,7 +442,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             break;
           }
           next_x = x + 1;
-          a = q[x];
+          a = base_at(x);
           if (a >= 4) {
             x = next_x;
             break;
@@ -395,7 +461,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             break;
           }
           next_x = j + 1;
-          a = q[j];
+          a = base_at(j);
           if (a >= 4) {
             x = next_x;
             st = P3_X;
@@ -531,6 +597,8 @@ struct gb_fmi_reads {
   int32_t nreads = 0, stride = 0;
   int lanes = 0;
   uint8_t *d_qdb = nullptr;
+  uint32_t *d_q4 = nullptr;
+  int32_t q4_stride = 0;
   int32_t *d_lens = nullptr;
   gbfmi::PEnt *d_scratch = nullptr;
   gb_smem *d_slots = nullptr;
@@ -633,6 +701,7 @@ int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes) {
 int gb_fmi_index_destroy(gb_fmi_index *idx) {
   if (!idx) return GB_OK;
   (void)hipFree(idx->d_occ);
+  (void)hipFree(idx->d_occ2);
   delete idx;
   return GB_OK;
 }
@@ -672,6 +741,15 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
   if (e == hipSuccess) e = hipMalloc(&R->d_temp, std::max<size_t>(R->temp_bytes, 16));
   if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
+  R->q4_stride = (max_readlength + 7) / 8;
+  if (e == hipSuccess) e = hipMalloc(&R->d_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
+  if (e == hipSuccess && num_reads) {
+    const int64_t nt = (int64_t)num_reads * R->q4_stride;
+    hipLaunchKernelGGL(gbfmi::pack_q4, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
+                       max_readlength, num_reads, R->q4_stride, R->d_q4);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(R->stream);
+  }
   if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_lens, lens, (size_t)num_reads * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     gb::set_error("gb_fmi_reads_create: %s", hipGetErrorString(e));
@@ -685,7 +763,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
 int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   if (!R) return GB_OK;
   if (R->stream) (void)hipStreamSynchronize(R->stream);
-  for (void *p : {(void *)R->d_qdb, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
+  for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
                   (void *)R->d_ovf_pos, (void *)R->d_big})
@@ -701,14 +779,25 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   GB_ARG(R, "gb_fmi_search: null read set");
   GB_ARG(min_seed_len > 0, "gb_fmi_search: min_seed_len %d", min_seed_len);
   GB_HIP(hipSetDevice(R->idx->device));
+  if (!R->idx->d_occ2) {  // search layout, built once per index
+    gb_fmi_index *ix = R->idx;
+    ix->cp2_size = (ix->n >> 7) + 1;
+    GB_HIP(hipMalloc(&ix->d_occ2, sizeof(gbfmi::Occ2) * (size_t)ix->cp2_size));
+    hipLaunchKernelGGL(gbfmi::compress_occ, dim3((unsigned)((ix->cp2_size + 255) / 256)), dim3(256), 0, R->stream,
+                       ix->d_occ, ix->cp_size, ix->d_occ2, ix->cp2_size);
+    GB_HIP(hipGetLastError());
+    GB_HIP(hipStreamSynchronize(R->stream));  // other read sets of this index may use other streams
+  }
   GB_HIP(hipEventRecord(R->ev[0], R->stream));
   GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
   GB_HIP(hipMemsetAsync(R->d_calls, 0, 2 * sizeof(unsigned long long), R->stream));
   gbfmi::SearchArgs A;
-  A.F.occ = R->idx->d_occ;
+  A.F.occ = R->idx->d_occ2;
   for (int b = 0; b < 5; b++) A.F.count[b] = R->idx->count[b];
   A.F.sentinel = R->idx->sentinel;
   A.qdb = R->d_qdb;
+  A.q4 = R->d_q4;
+  A.q4_stride = R->q4_stride;
   A.lens = R->d_lens;
   A.nreads = R->nreads;
   A.stride = R->stride;
@@ -732,7 +821,10 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
-    hipLaunchKernelGGL(gbfmi::smem_search, dim3(blocks), dim3(64), 0, R->stream, A);
+    if (R->stride <= gbfmi::kQBases)
+      hipLaunchKernelGGL(gbfmi::smem_search<true>, dim3(blocks), dim3(64), 0, R->stream, A);
+    else
+      hipLaunchKernelGGL(gbfmi::smem_search<false>, dim3(blocks), dim3(64), 0, R->stream, A);
     GB_HIP(hipGetLastError());
     hipLaunchKernelGGL(gbfmi::mark_overflow, dim3((gbfmi::kMaxOvf + 255) / 256), dim3(256), 0, R->stream,
                        R->d_ovf_list, R->d_ctl + 1, R->d_ovf_pos);

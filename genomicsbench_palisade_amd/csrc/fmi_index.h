@@ -13,6 +13,16 @@ struct __attribute__((aligned(64))) CpOcc {
 };
 static_assert(sizeof(CpOcc) == 64, "CP_OCC is 64 bytes");
 
+// Search-side layout, one 64-byte line per 128 BWT rows (half the reference table): the A, C and G
+// one-hot planes of the two 64-row blocks (same bit order as CP_OCC) and the occurrence counts of
+// A, C, G before the line packed as three 40-bit fields. T is derived: rows before p minus A, C, G
+// minus the sentinel row (which carries no base bit).
+struct __attribute__((aligned(64))) Occ2 {
+  uint64_t a[2], c[2], g[2];
+  uint64_t cnt[2];  // cA | cC << 40, cC >> 24 | cG << 16
+};
+static_assert(sizeof(Occ2) == 64, "Occ2 is 64 bytes");
+
 }  // namespace gbfmi
 
 // Index object behind the C ABI (one per device).
@@ -23,4 +33,6 @@ struct gb_fmi_index {
   int64_t sentinel = -1;
   int64_t cp_size = 0;      // (n >> 6) + 1 entries
   gbfmi::CpOcc *d_occ = nullptr;
+  int64_t cp2_size = 0;     // (n >> 7) + 1 lines
+  gbfmi::Occ2 *d_occ2 = nullptr;  // built from d_occ on first use
 };
