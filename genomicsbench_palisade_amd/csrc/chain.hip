@@ -84,6 +84,20 @@ __device__ __forceinline__ void compose_step(int32_t &a, int32_t &b) {
   b = max(ub + a, b);
   a = ua + a;
 }
+__device__ __forceinline__ int32_t scan_min(int32_t v) {
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xA, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xC, 0xF, false));
+  return v;
+}
+// number of set bits of m in lanes 0..lane (inclusive)
+__device__ __forceinline__ int32_t incl_count(uint64_t m, int lane) {
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  return below + (int)((m >> lane) & 1);
+}
 __device__ __forceinline__ void scan_compose(int32_t &a, int32_t &b) {
   compose_step<0x111, 0xF>(a, b);
   compose_step<0x112, 0xF>(a, b);
@@ -140,16 +154,20 @@ __device__ __forceinline__ int resolve_step(int32_t sc, bool ok, bool valid, int
   const int32_t mx = scan_max(ok ? sc : INT_MIN);  // inclusive max scan
   const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
   const bool upd = ok && sc > before;
-  int32_t a = upd ? -1 : ((ok && tgt) ? 1 : 0), b = 0;  // n -> max(n + a, b); n >= 0 always
-  scan_compose(a, b);
-  const int32_t n_after = max(N + a, b);
-  const bool brk = ok && !upd && tgt && n_after > kMaxSkip;
+  // n_skip after lane l as a reflected walk: steps +1 (target, no update), -1 floored at 0 (update),
+  // so n_l = max(N + D_l, D_l - min_{k<=l} D_k) with D_l the inclusive step sum -- D from two
+  // ballots and mbcnt, the running minimum from one DPP scan
+  const bool plus = ok && !upd && tgt;
+  const uint64_t pm = __ballot(plus), um_all = __ballot(upd);
+  const int32_t D = incl_count(pm, lane) - incl_count(um_all, lane);
+  const int32_t n_after = max(N + D, D - scan_min(D));
+  const bool brk = plus && n_after > kMaxSkip;
   const uint64_t bm = __ballot(brk);
   const int bl = bm ? __builtin_ctzll(bm) : 64;
   const int64_t nvalid = min((int64_t)64, jtop - st + 1);
   vis += (bl < 64) ? (unsigned long long)(bl + 1) : (unsigned long long)nvalid;
   const uint64_t low = bl >= 64 ? ~0ull : ((1ull << bl) - 1);
-  const uint64_t um = __ballot(upd) & low;
+  const uint64_t um = um_all & low;
   if (um) {
     const int lu = 63 - __builtin_clzll(um);
     J = jtop - lu;
