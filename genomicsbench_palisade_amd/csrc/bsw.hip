@@ -270,7 +270,7 @@ struct LaneArgs {
 };
 
 template <int NCH>
-__global__ __launch_bounds__(64) void bsw_lane_kernel(LaneArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 2 : 1))) void bsw_lane_kernel(LaneArgs A) {
   constexpr int NCOL = 8 * NCH;
   constexpr int NW = (NCOL + 31) / 32;
   const int lane = threadIdx.x;
