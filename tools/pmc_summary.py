@@ -12,26 +12,36 @@ import os
 import sys
 
 HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
-       "smem_search": "smem_search", "chain_kernel": "chain_kernel", "bsw_extend_kernel": "bsw_extend_kernel"}
+       "smem_search": "smem_search", "chain_kernel": "chain_kernel", "bsw_extend_kernel": "bsw_extend_kernel",
+       "bsw_lane_kernel": "bsw_lane_kernel"}
 
 
 def name_of(r):
     for k, v in HOT.items():
         if k in r["Kernel_Name"].replace(", ", "<").replace("(", "<"):
-            if v == "smem_search" and int(r["Grid_Size"]) <= 4096:
-                return "smem_search(pass 2)"
             return v
     return None
 
 
 def load(d):
+    """Per kernel name: one (bytes, ms) entry per dispatch; the variants of a multi-launch step
+    (bsw_lane_kernel<NCH>) are merged per step by summing consecutive dispatches of one step."""
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         n = name_of(r)
         if n:
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
-            out[n].append((float(r["Counter_Value"]) * 1024.0, dur))
-    return out
+            out[n].append((float(r["Counter_Value"]) * 1024.0, dur, r["Kernel_Name"]))
+    res = {}
+    for n, v in out.items():
+        variants = len(set(k for _, _, k in v))
+        if variants > 1:  # group dispatches into steps of `variants` launches
+            v = [(sum(b for b, _, _ in v[i:i + variants]), sum(t for _, t, _ in v[i:i + variants]))
+                 for i in range(0, len(v) - variants + 1, variants)]
+        else:
+            v = [(b, t) for b, t, _ in v]
+        res[n] = v
+    return res
 
 
 def main():
