@@ -148,10 +148,6 @@ __device__ __forceinline__ int dpp_shr(int v, int lane0) {
   // wave_shr:1 (DPP ctrl 0x138); lane 0 has no source lane and keeps `lane0` (bound_ctrl off).
   return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);
 }
-__device__ __forceinline__ int dpp_shl(int v, int lane63) {
-  // wave_shl:1 (DPP ctrl 0x130); lane 63 has no source lane and keeps `lane63`.
-  return __builtin_amdgcn_update_dpp(lane63, v, 0x130, 0xF, 0xF, false);
-}
 template <int (*F)(int, int)>
 __device__ __forceinline__ float dpp(float v, float keep) {
   return __builtin_bit_cast(float, F(__builtin_bit_cast(int, v), __builtin_bit_cast(int, keep)));
@@ -196,7 +192,6 @@ struct RowParams {
 template <typename T>
 struct LaneState {
   T Mp, Yp, zo, wo, zd;
-  T cz, cw;  // collectors: lane j holds lane 63's z/w of 63-j steps ago (stripe boundary writer)
 };
 
 // One anti-diagonal step. Arithmetic per cell is exactly the reference's (no FMA, same order):
@@ -205,7 +200,7 @@ struct LaneState {
 //   Y = M[r][c-1]*pMY + Y[r][c-1]*pYY
 template <typename T, bool kLast>
 __device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneState<T> &st,
-                                          const RowParams<T> &P, T &sumM, T &sumX) {
+                                          const RowParams<T> &P, T &sumM, T &sumX, Brec<T> *wr, bool last_lane) {
   const T X = dpp<dpp_shr>(st.wo, rec.w);          // X[r][c]
   const T zdn = dpp<dpp_shr>(st.zo, rec.z);        // bracket for column c+1
   const T dist = select_dist(P.rmask, h, P.dmatch, P.dmis);
@@ -217,28 +212,22 @@ __device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneSt
     sumM = sumM + M;
     sumX = sumX + X;
   } else {
-    st.cz = dpp<dpp_shl>(st.cz, st.zo);
-    st.cw = dpp<dpp_shl>(st.cw, st.wo);
+    // lane 63 hands its row's z/w (the next stripe's brackets) to LDS; columns < 1 land in the pad
+    if (last_lane) {
+      Brec<T> b;
+      b.z = st.zo;
+      b.w = st.wo;
+      *wr = b;
+    }
   }
   st.zd = zdn;
   st.Mp = M;
   st.Yp = Y;
 }
 
-// Lane j of the collectors holds lane 63's z/w of step t-63+j, i.e. column t-125+j of the row
-// below this stripe; write the ones that are real columns.
-template <typename T>
-__device__ __forceinline__ void flush_boundary(const LaneState<T> &st, Brec<T> *__restrict__ bnd, int t,
-                                               int C, int lane) {
-  const int c = t - 125 + lane;
-  if (c >= 1 && c <= C) {
-    bnd[c].z = st.cz;
-    bnd[c].w = st.cw;
-  }
-}
-
 // Sweep `steps` anti-diagonals of one stripe, 4 per iteration, the boundary records of the next
-// block prefetched before this block runs (reads are at columns > t, boundary writes at <= t-62).
+// block prefetched before this block runs. Reads are at columns > t; lane 63 writes column t-62 of
+// the row below at step t (bnd has kWave pad records below column 0 for the first 62 steps).
 template <typename T, bool kLast>
 __device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const RowParams<T> &P,
                                             T &sumM, T &sumX, Brec<T> *__restrict__ bnd,
@@ -246,6 +235,7 @@ __device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const R
   // hcol[c] = haplotype code of column c (valid for c in [-63, C+kBndPad)); lane's column at step
   // t is t - lane + 1.
   const uint8_t *hl = hcol + 1 - lane;
+  const bool last_lane = lane == kWave - 1;
   constexpr int U = 4;
   int t = 0;
   for (; t + U <= steps; t += U) {
@@ -253,16 +243,14 @@ __device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const R
     // covered by the other waves on the SIMD
     const Brec<T> c0 = bnd[t + 1], c1 = bnd[t + 2], c2 = bnd[t + 3], c3 = bnd[t + 4];
     const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
-    phmm_step<T, kLast>(c0, h0, st, P, sumM, sumX);
-    phmm_step<T, kLast>(c1, h1, st, P, sumM, sumX);
-    phmm_step<T, kLast>(c2, h2, st, P, sumM, sumX);
-    phmm_step<T, kLast>(c3, h3, st, P, sumM, sumX);
-    if constexpr (!kLast) {
-      if (((t + U) & (kWave - 1)) == 0) flush_boundary(st, bnd, t + U - 1, C, lane);
-    }
+    Brec<T> *wr = bnd + (t - (kWave - 2));
+    phmm_step<T, kLast>(c0, h0, st, P, sumM, sumX, wr, last_lane);
+    phmm_step<T, kLast>(c1, h1, st, P, sumM, sumX, wr + 1, last_lane);
+    phmm_step<T, kLast>(c2, h2, st, P, sumM, sumX, wr + 2, last_lane);
+    phmm_step<T, kLast>(c3, h3, st, P, sumM, sumX, wr + 3, last_lane);
   }
-  for (; t < steps; t++) phmm_step<T, kLast>(bnd[t + 1], hl[t], st, P, sumM, sumX);
-  if constexpr (!kLast) flush_boundary(st, bnd, steps - 1, C, lane);
+  for (; t < steps; t++)
+    phmm_step<T, kLast>(bnd[t + 1], hl[t], st, P, sumM, sumX, bnd + (t - (kWave - 2)), last_lane);
 }
 
 template <typename T>
@@ -308,8 +296,8 @@ __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ de
   const uint8_t *rbase = pool + desc.read_off;
   // LDS: boundary records for columns [0, C+kBndPad), then haplotype codes for columns
   // [-kWave, C+kBndPad) (codes 0 outside 1..C; cells outside the matrix never feed real cells).
-  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw);
-  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad) + kWave;
+  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw) + kWave;  // kWave pad records below column 0
+  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad + kWave) + kWave;
 
   // Row 0 -> first row's partials: M = X = 0, Y = init_Y, so z = (0*pMM + 0*pGAPM) + init_Y*pGAPM
   // (evaluated, not simplified, to keep the reference's operation order) and w = 0*pMX + 0*pXX.
@@ -349,7 +337,6 @@ __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ de
     LaneState<T> st;
     st.Mp = st.Yp = st.zo = st.wo = (T)0;
     st.zd = (lane == 0) ? bnd[0].z : (T)0;  // bracket at column 0: z0 for stripe 0, 0 below
-    st.cz = st.cw = (T)0;
     T sumM = (T)0, sumX = (T)0;
     if (s == nstripes - 1) {
       phmm_stripe<T, true>(C + nrows - 1, st, P, sumM, sumX, bnd, hcol, C, lane);
@@ -622,8 +609,8 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipMemsetAsync(b->d_count, 0, sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
-    const size_t lds_f = (sizeof(Brec<float>) + 1) * (size_t)(b->max_haplen + kBndPad) + kWave + 16;
-    const size_t lds_d = (sizeof(Brec<double>) + 1) * (size_t)(b->max_haplen + kBndPad) + kWave + 16;
+    const size_t lds_f = (sizeof(Brec<float>) + 1) * (size_t)(b->max_haplen + kBndPad) + sizeof(Brec<float>) * kWave + kWave + 16;
+    const size_t lds_d = (sizeof(Brec<double>) + 1) * (size_t)(b->max_haplen + kBndPad) + sizeof(Brec<double>) * kWave + kWave + 16;
     if (!b->force_f64) {
       hipLaunchKernelGGL((phmm_forward<float, false>), dim3(n), dim3(kWave), lds_f, b->stream,
                          b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,
