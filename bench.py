@@ -37,6 +37,8 @@ PEAK_F64_OPS = PEAK_F32_OPS / 2      # FP64 vector peak 78.6 TF (FMA=2) -> 39.3e
 PHMM_FLOP_PER_CELL = 12              # 12 FP ops per cell, no FMA
 PEAK_HBM = 8.0e12                    # HBM3E spec bytes/s (MI355X_MICROARCH.md)
 FMI_BYTES_PER_EXT = 128              # 2 x 64-B CP_OCC lines per backwardExt
+SA_BYTES_PER_STEP = 64               # one 64-B Occ2 line per LF step of an SA lookup
+SA_BYTES_PER_COORD = 24              # row in, sampled-SA entry, coordinate out (8 B each)
 CHAIN_OPS_PER_PAIR = 25              # ~25 int32/fp64 ops per visited (i, j) pair
 PEAK_CHAIN_OPS = PEAK_F64_OPS        # INT32/FP64 VALU, 39.3e12 lane-op/s
 BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar inner-loop iteration
@@ -452,6 +454,7 @@ def bench_fmi(args, D, rank, world):
         cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds)
         oi.close()
     n, _, _ = idx.info()
+    sa = bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens)
     rs.close()
     idx.close()
     return {
@@ -465,7 +468,77 @@ def bench_fmi(args, D, rank, world):
                      "algorithmic_bytes": int(alg_bytes)},
         "kernels_ms": {"smem_search": ms, "smem_search+scan": float(np.mean(kt))},
         "cpu_baseline": cpu,
+        "sa_lookup": sa,
     }
+
+
+def bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens):
+    """SA coordinates of every SMEM of the last search (get_sa_entries_prefetch, max_occ 500, i.e.
+    bwamem.cpp:737 over every read). A step = row expansion + all LF walks."""
+    log("fmi: SA lookup")
+    for _ in range(max(1, args.warmup)):
+        rs.sa_run(fmi.MAX_OCC, fmi.SA_PREFETCH)
+        rs.sync()
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    kms = []
+    steps = ncoords = 0
+    for _ in range(args.steps):
+        rs.sa_run(fmi.MAX_OCC, fmi.SA_PREFETCH)
+        rs.sync()
+        a, steps, ncoords = rs.sa_timing()
+        kms.append(a)
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    mcoords = D.sum(float(ncoords)) * args.steps / elapsed / 1e6
+    ms = float(np.mean(kms))
+    # per coordinate: its row (8 B read), one sampled-SA entry (8 B), the coordinate (8 B written);
+    # per LF step one 64-B Occ2 line
+    alg_bytes = steps * SA_BYTES_PER_STEP + ncoords * SA_BYTES_PER_COORD
+    ach = alg_bytes / (ms * 1e-3)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import fmi_util
+        n_, c_, s_ = idx.info()
+        oi = fmi_util.OracleIndex(adopt=(n_, c_, s_, idx.cp_occ(), idx.sampled_sa()))
+        log("fmi: SA CPU baseline")
+        cpu = cpu_baseline_sa(oi, codes, lens, args.cpu_seconds)
+        oi.close()
+    return {
+        "value": round(mcoords, 3), "unit": "Mcoords/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": "SA coordinates of every SMEM of the fmi shard (get_sa_entries_prefetch, "
+                               "max_occ 500, sampled SA every 8 rows)",
+                   "coords_per_step": int(ncoords), "lf_steps_per_coord": steps / max(ncoords, 1)},
+        "roofline": {"bound": "hbm", "kernel": "sa_walk", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
+                     "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": pmc_traffic("sa_walk"),
+                     "algorithmic_bytes": int(alg_bytes)},
+        "kernels_ms": {"sa_expand+sa_walk": ms},
+        "cpu_baseline": cpu,
+    }
+
+
+def cpu_baseline_sa(oi, codes, lens, sample_seconds: float):
+    """The C restatement of get_sa_entries_prefetch (oracle/fmi_oracle.c, kind 'port') over the SMEMs of
+    the first reads of the same shard (found by the oracle's own search), threads over SMEM ranges."""
+    threads = max(1, min(16, _cores()))
+    m = min(len(lens), 20000)
+    sm, _, _ = oi.run(codes[:m], lens[:m], batch_size=512)
+    t0 = time.perf_counter()
+    tot, _ = oi.sa_entries_threaded(sm, threads)
+    t = time.perf_counter() - t0
+    reps = 1
+    if t < sample_seconds / 4 and t > 0:
+        reps = max(1, int(sample_seconds / 2 / t))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oi.sa_entries_threaded(sm, threads)
+        t = time.perf_counter() - t0
+    return {"value": tot * reps / t / 1e6, "unit": "Mcoords/s", "cores": threads, "kind": "port",
+            "sample": f"SA coordinates of the {len(sm)} SMEMs of the first {m} reads of the same shard "
+                      f"(max_occ 500), {reps} pass(es) over {threads} threads, {t:.1f} s"}
 
 
 def main():

@@ -615,6 +615,9 @@ struct gb_fmi_reads {
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
   bool ran = false;
+  bool scattered = false;  // d_out holds the last search's compacted SMEMs
+  int64_t total = 0;
+  gbfmi::SaJob *sa = nullptr;
 };
 
 namespace {
@@ -630,6 +633,79 @@ int lanes_for_device() {
 }
 
 }  // namespace
+
+namespace gbfmi {
+
+int ensure_occ2(gb_fmi_index *ix, hipStream_t s) {
+  if (ix->d_occ2) return GB_OK;
+  ix->cp2_size = (ix->n >> 7) + 1;
+  GB_HIP(hipMalloc(&ix->d_occ2, sizeof(Occ2) * (size_t)ix->cp2_size));
+  hipLaunchKernelGGL(compress_occ, dim3((unsigned)((ix->cp2_size + 255) / 256)), dim3(256), 0, s, ix->d_occ,
+                     ix->cp_size, ix->d_occ2, ix->cp2_size);
+  GB_HIP(hipGetLastError());
+  GB_HIP(hipStreamSynchronize(s));  // other read sets of this index may use other streams
+  return GB_OK;
+}
+
+hipStream_t reads_stream(gb_fmi_reads *R) { return R->stream; }
+gb_fmi_index *reads_index(gb_fmi_reads *R) { return R->idx; }
+SaJob **reads_sa_job(gb_fmi_reads *R) { return &R->sa; }
+
+namespace {
+int check_fatal(gb_fmi_reads *R, const char *who) {
+  int32_t ctl[4];
+  GB_HIP(hipMemcpy(ctl, R->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+  if (ctl[2] != 0) {
+    gb::set_error("%s: %d reads exceeded %d SMEM slots (or more than %d reads exceeded %d)", who, ctl[2], kBigCap,
+                  kMaxOvf, kCap);
+    return GB_ERR_STATE;
+  }
+  return GB_OK;
+}
+
+// Compact the slots into d_out (exclusive scan already in d_offsets); tot = total SMEMs.
+int scatter_out(gb_fmi_reads *R, int64_t tot) {
+  if (!R->scattered) {
+    if (tot > R->out_cap) {
+      (void)hipFree(R->d_out);
+      R->d_out = nullptr;
+      GB_HIP(hipMalloc(&R->d_out, sizeof(gb_smem) * (size_t)tot));
+      R->out_cap = tot;
+    }
+    if (tot) {
+      hipLaunchKernelGGL(scatter_smems, dim3((R->nreads + 255) / 256), dim3(256), 0, R->stream, R->d_slots, R->d_big,
+                         R->d_ovf_pos, R->d_counts, R->d_offsets, R->d_out, R->nreads);
+      GB_HIP(hipGetLastError());
+    }
+    R->scattered = true;
+    R->total = tot;
+  }
+  return GB_OK;
+}
+}  // namespace
+
+int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n) {
+  GB_ARG(R && R->ran, "SA lookup: the read set has not been searched");
+  GB_HIP(hipSetDevice(R->idx->device));
+  GB_HIP(hipStreamSynchronize(R->stream));
+  int st = check_fatal(R, "SA lookup");
+  if (st) return st;
+  int64_t tot = 0;
+  if (R->nreads > 0) {
+    int64_t last_off = 0;
+    int32_t last_cnt = 0;
+    GB_HIP(hipMemcpy(&last_off, R->d_offsets + (R->nreads - 1), sizeof(int64_t), hipMemcpyDeviceToHost));
+    GB_HIP(hipMemcpy(&last_cnt, R->d_counts + (R->nreads - 1), sizeof(int32_t), hipMemcpyDeviceToHost));
+    tot = last_off + last_cnt;
+  }
+  if ((st = scatter_out(R, tot))) return st;
+  GB_HIP(hipStreamSynchronize(R->stream));
+  *d_smems = R->d_out;
+  *n = R->total;
+  return GB_OK;
+}
+
+}  // namespace gbfmi
 
 extern "C" {
 
@@ -656,25 +732,35 @@ int gb_fmi_index_load(const char *path, gb_fmi_index **out) {
   }
   const int64_t ns = (n >> 3) + 1;  // SA_COMPRESSION with SA_COMPX = 3 (macro.h:64-66)
   int64_t sentinel = -1;
-  if (fseek(fp, ns * 5, SEEK_CUR) != 0 || fread(&sentinel, 8, 1, fp) != 1) {
+  std::vector<int8_t> ms((size_t)ns);
+  std::vector<uint32_t> ls((size_t)ns);
+  if (fread(ms.data(), 1, (size_t)ns, fp) != (size_t)ns || fread(ls.data(), 4, (size_t)ns, fp) != (size_t)ns ||
+      fread(&sentinel, 8, 1, fp) != 1) {
     fclose(fp);
     gb::set_error("gb_fmi_index_load: %s: truncated (sampled SA / sentinel)", path);
     return GB_ERR_ARG;
   }
   fclose(fp);
+  // sa_entry = sa_ms_byte << 32 + sa_ls_word (FMI_search.cpp:1790-1802), packed once at load
+  std::vector<int64_t> sa((size_t)ns);
+  for (int64_t i = 0; i < ns; i++) sa[i] = ((int64_t)ms[i] << 32) + (int64_t)ls[i];
+  std::vector<int8_t>().swap(ms);
+  std::vector<uint32_t>().swap(ls);
   auto *idx = new gb_fmi_index();
   GB_HIP(hipGetDevice(&idx->device));
   idx->n = n;
   for (int b = 0; b < 5; b++) idx->count[b] = count[b] + 1;  // FMI_search.cpp:763-768
   idx->sentinel = sentinel;
   idx->cp_size = cp_size;
+  idx->sa_ns = ns;
   hipError_t e = hipMalloc(&idx->d_occ, sizeof(gbfmi::CpOcc) * (size_t)cp_size);
   if (e == hipSuccess)
     e = hipMemcpy(idx->d_occ, occ.data(), sizeof(gbfmi::CpOcc) * (size_t)cp_size, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&idx->d_sa, sizeof(int64_t) * (size_t)ns);
+  if (e == hipSuccess) e = hipMemcpy(idx->d_sa, sa.data(), sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     gb::set_error("gb_fmi_index_load: %s", hipGetErrorString(e));
-    (void)hipFree(idx->d_occ);
-    delete idx;
+    gb_fmi_index_destroy(idx);
     return GB_ERR_HIP;
   }
   *out = idx;
@@ -698,10 +784,19 @@ int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes) {
   return GB_OK;
 }
 
+int gb_fmi_index_sa(gb_fmi_index *idx, int64_t *dst, int64_t dst_entries) {
+  GB_ARG(idx && dst, "gb_fmi_index_sa: null argument");
+  GB_ARG(idx->d_sa, "gb_fmi_index_sa: index has no sampled suffix array");
+  GB_ARG(dst_entries >= idx->sa_ns, "gb_fmi_index_sa: need %lld entries", (long long)idx->sa_ns);
+  GB_HIP(hipMemcpy(dst, idx->d_sa, sizeof(int64_t) * (size_t)idx->sa_ns, hipMemcpyDeviceToHost));
+  return GB_OK;
+}
+
 int gb_fmi_index_destroy(gb_fmi_index *idx) {
   if (!idx) return GB_OK;
   (void)hipFree(idx->d_occ);
   (void)hipFree(idx->d_occ2);
+  (void)hipFree(idx->d_sa);
   delete idx;
   return GB_OK;
 }
@@ -763,6 +858,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
 int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   if (!R) return GB_OK;
   if (R->stream) (void)hipStreamSynchronize(R->stream);
+  gbfmi::sa_job_destroy(R->sa);
   for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
@@ -779,15 +875,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   GB_ARG(R, "gb_fmi_search: null read set");
   GB_ARG(min_seed_len > 0, "gb_fmi_search: min_seed_len %d", min_seed_len);
   GB_HIP(hipSetDevice(R->idx->device));
-  if (!R->idx->d_occ2) {  // search layout, built once per index
-    gb_fmi_index *ix = R->idx;
-    ix->cp2_size = (ix->n >> 7) + 1;
-    GB_HIP(hipMalloc(&ix->d_occ2, sizeof(gbfmi::Occ2) * (size_t)ix->cp2_size));
-    hipLaunchKernelGGL(gbfmi::compress_occ, dim3((unsigned)((ix->cp2_size + 255) / 256)), dim3(256), 0, R->stream,
-                       ix->d_occ, ix->cp_size, ix->d_occ2, ix->cp2_size);
-    GB_HIP(hipGetLastError());
-    GB_HIP(hipStreamSynchronize(R->stream));  // other read sets of this index may use other streams
-  }
+  if (int st = gbfmi::ensure_occ2(R->idx, R->stream)) return st;
   GB_HIP(hipEventRecord(R->ev[0], R->stream));
   GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
   GB_HIP(hipMemsetAsync(R->d_calls, 0, 2 * sizeof(unsigned long long), R->stream));
@@ -837,6 +925,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   }
   GB_HIP(hipEventRecord(R->ev[2], R->stream));
   R->ran = true;
+  R->scattered = false;
   return GB_OK;
 }
 
@@ -852,13 +941,7 @@ int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t ou
   GB_ARG(batch_size > 0, "gb_fmi_results: batch_size %d", batch_size);
   GB_HIP(hipSetDevice(R->idx->device));
   GB_HIP(hipStreamSynchronize(R->stream));
-  int32_t ctl[4];
-  GB_HIP(hipMemcpy(ctl, R->d_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
-  if (ctl[2] != 0) {
-    gb::set_error("gb_fmi_results: %d reads exceeded %d SMEM slots (or more than %d reads exceeded %d)",
-                  ctl[2], gbfmi::kBigCap, gbfmi::kMaxOvf, gbfmi::kCap);
-    return GB_ERR_STATE;
-  }
+  if (int st = gbfmi::check_fatal(R, "gb_fmi_results")) return st;
   const int32_t n = R->nreads;
   std::vector<int32_t> counts((size_t)std::max(n, 1)), phase((size_t)std::max(n, 1) * 3);
   if (n) {
@@ -882,16 +965,8 @@ int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t ou
   }
   if (out) {
     GB_ARG(out_cap >= tot, "gb_fmi_results: out_cap %lld < %lld SMEMs", (long long)out_cap, (long long)tot);
-    if (tot > R->out_cap) {
-      (void)hipFree(R->d_out);
-      R->d_out = nullptr;
-      GB_HIP(hipMalloc(&R->d_out, sizeof(gb_smem) * (size_t)tot));
-      R->out_cap = tot;
-    }
+    if (int st = gbfmi::scatter_out(R, tot)) return st;
     if (tot) {
-      hipLaunchKernelGGL(gbfmi::scatter_smems, dim3((n + 255) / 256), dim3(256), 0, R->stream,
-                         R->d_slots, R->d_big, R->d_ovf_pos, R->d_counts, R->d_offsets, R->d_out, n);
-      GB_HIP(hipGetLastError());
       GB_HIP(hipMemcpyAsync(out, R->d_out, sizeof(gb_smem) * (size_t)tot, hipMemcpyDeviceToHost, R->stream));
       GB_HIP(hipStreamSynchronize(R->stream));
     }

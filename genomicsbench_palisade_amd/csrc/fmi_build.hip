@@ -142,8 +142,9 @@ __global__ void find_sentinel(const uint32_t *__restrict__ sa, int64_t N, int64_
   if (j < N && sa[j] == 0) *out = j + 1;
 }
 
+// sampled SA every 8th row (SA_COMPX = 3): file layout (ms byte, ls word) and the packed search copy
 __global__ void sample_sa(const uint32_t *__restrict__ sa, int64_t N, int64_t ns, int8_t *__restrict__ ms,
-                          uint32_t *__restrict__ ls) {
+                          uint32_t *__restrict__ ls, int64_t *__restrict__ sa64) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ns) return;
   const int64_t r = p << 3;
@@ -152,8 +153,13 @@ __global__ void sample_sa(const uint32_t *__restrict__ sa, int64_t N, int64_t ns
     v = N;
   else if (r <= N)
     v = sa[r - 1];
-  ls[p] = (uint32_t)(v & 0xffffffff);
-  ms[p] = (int8_t)((v >> 32) & 0xff);
+  const int8_t hi = (int8_t)((v >> 32) & 0xff);
+  const uint32_t lo = (uint32_t)(v & 0xffffffff);
+  if (ms) {
+    ls[p] = lo;
+    ms[p] = hi;
+  }
+  sa64[p] = ((int64_t)hi << 32) + (int64_t)lo;
 }
 
 inline unsigned grid(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
@@ -337,15 +343,28 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
   idx->sentinel = sentinel;
   idx->cp_size = nblocks;
 
-  // (4) optional reference-format file (build_fm_index, FMI_search.cpp:206-347)
-  if (out_path) {
-    const int64_t ns = (n >> 3) + 1;
+  // (4) sampled SA kept on the device for SA lookups; optional reference-format file
+  //     (build_fm_index, FMI_search.cpp:206-347)
+  const int64_t ns = (n >> 3) + 1;
+  idx->sa_ns = ns;
+  if (hipMalloc(&idx->d_sa, sizeof(int64_t) * (size_t)ns) != hipSuccess) {
+    gb_fmi_index_destroy(idx);
+    gb::set_error("gb_fmi_index_build: out of device memory (sampled SA)");
+    return GB_ERR_HIP;
+  }
+  if (!out_path) {
+    hipLaunchKernelGGL(sample_sa, dim3(grid(ns)), dim3(256), 0, s, sa, N, ns, (int8_t *)nullptr, (uint32_t *)nullptr,
+                       idx->d_sa);
+    GB_HIPX(hipGetLastError());
+    GB_HIPX(hipDeviceSynchronize());
+  } else {
     DevBuf d_ms, d_ls;
     if ((st = dalloc<int8_t>(d_ms, ns)) || (st = dalloc<uint32_t>(d_ls, ns))) {
       gb_fmi_index_destroy(idx);
       return st;
     }
-    hipLaunchKernelGGL(sample_sa, dim3(grid(ns)), dim3(256), 0, s, sa, N, ns, d_ms.as<int8_t>(), d_ls.as<uint32_t>());
+    hipLaunchKernelGGL(sample_sa, dim3(grid(ns)), dim3(256), 0, s, sa, N, ns, d_ms.as<int8_t>(), d_ls.as<uint32_t>(),
+                       idx->d_sa);
     std::vector<CpOcc> occ((size_t)nblocks);
     std::vector<int8_t> ms((size_t)ns);
     std::vector<uint32_t> ls((size_t)ns);

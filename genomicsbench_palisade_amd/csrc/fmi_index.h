@@ -35,4 +35,22 @@ struct gb_fmi_index {
   gbfmi::CpOcc *d_occ = nullptr;
   int64_t cp2_size = 0;     // (n >> 7) + 1 lines
   gbfmi::Occ2 *d_occ2 = nullptr;  // built from d_occ on first use
+  int64_t sa_ns = 0;        // (n >> 3) + 1 sampled SA entries (SA_COMPX = 3, macro.h:64-66)
+  int64_t *d_sa = nullptr;  // sa_ms_byte << 32 + sa_ls_word, one int64 per sampled row
 };
+
+struct gb_fmi_reads;
+struct gb_smem;
+
+namespace gbfmi {
+// fmi.hip: the search-side Occ2 table (built once per index, on `s`).
+int ensure_occ2(gb_fmi_index *ix, hipStream_t s);
+// fmi.hip: the last search's SMEMs compacted on the device in (rid, m, n desc) order.
+int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n);
+hipStream_t reads_stream(gb_fmi_reads *R);
+gb_fmi_index *reads_index(gb_fmi_reads *R);
+// fmi_sa.hip: per-read-set SA-lookup state, released with the read set.
+struct SaJob;
+void sa_job_destroy(SaJob *j);
+SaJob **reads_sa_job(gb_fmi_reads *R);
+}  // namespace gbfmi

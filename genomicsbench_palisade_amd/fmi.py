@@ -1,6 +1,7 @@
 """Host mirror of the reference FMI_search interface (tools/bwa-mem2/src/FMI_search.h:101-224) and
 the fmi benchmark pipeline (benchmarks/fmi/fmi.cpp:253-348), executed by the HIP kernels in
-libgb.so (csrc/fmi.hip, csrc/fmi_build.hip)."""
+libgb.so (csrc/fmi.hip, csrc/fmi_build.hip, csrc/fmi_sa.hip). SA lookup: get_sa_entry_compressed /
+get_sa_entries_prefetch (FMI_search.cpp:1714-2040)."""
 from __future__ import annotations
 
 import ctypes
@@ -8,6 +9,10 @@ import ctypes
 import numpy as np
 
 from . import check, lib
+
+SA_COMPRESSED = 0  # get_sa_entry_compressed (FMI_search.cpp:1714-1807)
+SA_PREFETCH = 1    # get_sa_entries_prefetch / call_one_step (:1834-2040), what bwamem.cpp:737 calls
+MAX_OCC = 500      # bwa-mem2's default opt->max_occ
 
 SMEM_DTYPE = np.dtype([("rid", "<u4"), ("m", "<u4"), ("n", "<u4"), ("pad", "<u4"),
                        ("k", "<i8"), ("l", "<i8"), ("s", "<i8")])  # == SMEM (FMI_search.h:91-99)
@@ -29,6 +34,12 @@ def _decl():
     L.gb_fmi_sync.argtypes = [vp]
     L.gb_fmi_results.argtypes = [vp, i32, vp, i64, vp, vp, vp]
     L.gb_fmi_timing.argtypes = [vp, vp, vp, vp]
+    L.gb_fmi_index_sa.argtypes = [vp, vp, i64]
+    L.gb_fmi_sa_lookup.argtypes = [vp, vp, i64, i32, vp]
+    L.gb_fmi_sa_entries.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, vp]
+    L.gb_fmi_reads_sa_run.argtypes = [vp, i32, i32]
+    L.gb_fmi_reads_sa_results.argtypes = [vp, vp, i64, vp, vp]
+    L.gb_fmi_reads_sa_timing.argtypes = [vp, vp, vp, vp]
     L._fmi_decl = True
     return L
 
@@ -67,6 +78,33 @@ class Index:
         buf = np.zeros(size * 8, np.int64)
         check(_decl().gb_fmi_index_cp_occ(self.h, buf.ctypes.data, buf.nbytes), "gb_fmi_index_cp_occ")
         return buf.reshape(size, 8)
+
+    def sampled_sa(self):
+        n, _, _ = self.info()
+        buf = np.zeros((n >> 3) + 1, np.int64)
+        check(_decl().gb_fmi_index_sa(self.h, buf.ctypes.data, len(buf)), "gb_fmi_index_sa")
+        return buf
+
+    def sa_lookup(self, rows, mode: int = SA_PREFETCH) -> np.ndarray:
+        """SA value of each BWT row (one LF walk per row on the GPU)."""
+        rows = np.ascontiguousarray(rows, np.int64)
+        out = np.zeros(max(len(rows), 1), np.int64)
+        check(_decl().gb_fmi_sa_lookup(self.h, rows.ctypes.data, len(rows), mode, out.ctypes.data),
+              "gb_fmi_sa_lookup")
+        return out[:len(rows)]
+
+    def sa_entries(self, smems, max_occ: int = MAX_OCC, mode: int = SA_PREFETCH):
+        """get_sa_entries(_prefetch) over an SMEM array -> (coords, per-SMEM counts)."""
+        smems = np.ascontiguousarray(smems, SMEM_DTYPE)
+        n = len(smems)
+        cap = int(np.minimum(np.maximum(smems["s"], 0), max_occ).sum()) if n else 0
+        coords = np.zeros(max(cap, 1), np.int64)
+        counts = np.zeros(max(n, 1), np.int32)
+        tot = ctypes.c_int64()
+        check(_decl().gb_fmi_sa_entries(self.h, smems.ctypes.data, n, max_occ, mode, coords.ctypes.data,
+                                        len(coords), counts.ctypes.data, ctypes.byref(tot)),
+              "gb_fmi_sa_entries")
+        return coords[:tot.value], counts[:n]
 
     def close(self):
         if self.h:
@@ -121,6 +159,31 @@ class Reads:
         check(_decl().gb_fmi_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
               "gb_fmi_timing")
         return a.value, b.value, c.value
+
+    def sa_run(self, max_occ: int = MAX_OCC, mode: int = SA_PREFETCH):
+        """SA coordinates of the last search's SMEMs, on the device (bwamem.cpp:737 for every read)."""
+        check(_decl().gb_fmi_reads_sa_run(self.h, max_occ, mode), "gb_fmi_reads_sa_run")
+
+    def sa_results(self, want_coords: bool = True):
+        L = _decl()
+        tot = ctypes.c_int64()
+        check(L.gb_fmi_reads_sa_results(self.h, None, 0, None, ctypes.byref(tot)), "gb_fmi_reads_sa_results")
+        if not want_coords:
+            return None, None, tot.value
+        coords = np.zeros(max(tot.value, 1), np.int64)
+        _, ns, _, _ = self.results(want_smems=False)
+        counts = np.zeros(max(ns, 1), np.int32)
+        check(L.gb_fmi_reads_sa_results(self.h, coords.ctypes.data, len(coords), counts.ctypes.data, None),
+              "gb_fmi_reads_sa_results")
+        return coords[:tot.value], counts[:ns], tot.value
+
+    def sa_timing(self):
+        """(kernel ms, LF steps, coordinates) of the last sa_run."""
+        a = ctypes.c_float()
+        st, nc = ctypes.c_int64(), ctypes.c_int64()
+        check(_decl().gb_fmi_reads_sa_timing(self.h, ctypes.byref(a), ctypes.byref(st), ctypes.byref(nc)),
+              "gb_fmi_reads_sa_timing")
+        return a.value, st.value, nc.value
 
     def close(self):
         if self.h:

@@ -46,6 +46,8 @@ int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, const char *ou
 int gb_fmi_index_info(gb_fmi_index *idx, int64_t *n, int64_t *count5, int64_t *sentinel_index);
 /* Copies the CP_OCC table (64 bytes per 64 BWT rows, reference layout) to host memory. */
 int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes);
+/* Copies the packed sampled SA ((n >> 3) + 1 int64 entries, sa_ms_byte << 32 + sa_ls_word) to host. */
+int gb_fmi_index_sa(gb_fmi_index *idx, int64_t *dst, int64_t dst_entries);
 int gb_fmi_index_destroy(gb_fmi_index *idx);
 
 /* Device-resident read set: enc_qdb is numReads x max_readlength codes (A0 C1 G2 T3, else 4;
@@ -67,6 +69,32 @@ int gb_fmi_results(gb_fmi_reads *r, int32_t batch_size, gb_smem *out, int64_t ou
 /* Kernel time of the last search (HIP events on the read set's stream), ms; backwardExt calls. */
 int gb_fmi_timing(gb_fmi_reads *r, float *search_ms, float *total_ms, int64_t *bwt_calls);
 int gb_fmi_sync(gb_fmi_reads *r);
+
+/* ---- SA lookup: BWT rows -> reference coordinates (sampled SA every 8th row, SA_COMPX 3,
+ *      macro.h:64-66; loaded from the index file / kept from gb_fmi_index_build).
+ * GB_FMI_SA_COMPRESSED  FMI_search::get_sa_entry_compressed   FMI_search.cpp:1714-1807
+ * GB_FMI_SA_PREFETCH    FMI_search::get_sa_entries_prefetch + call_one_step
+ *                       FMI_search.cpp:1834-2040, the variant the aligner calls (bwamem.cpp:737);
+ *                       differs from the above only when the LF walk reaches the sentinel row after
+ *                       one or more steps: it answers 0 there (:1865-1869) instead of the step count. */
+#define GB_FMI_SA_COMPRESSED 0
+#define GB_FMI_SA_PREFETCH 1
+/* SA value of each row rows[0..n) (0 <= row < n_index) into out[0..n). */
+int gb_fmi_sa_lookup(gb_fmi_index *idx, const int64_t *rows, int64_t n, int32_t mode, int64_t *out);
+/* get_sa_entries(_prefetch) (FMI_search.cpp:1596-1619 / :1895-1931) over n host SMEMs: SMEM i
+ * contributes the SA values of rows k, k+step, ... (< k+s, at most max_occ of them), step =
+ * s > max_occ ? s / max_occ : 1, concatenated in SMEM order into coords; counts[i] (nullable) = that
+ * number; *total = sum. max_occ > 0 (bwa-mem2's default is 500). */
+int gb_fmi_sa_entries(gb_fmi_index *idx, const gb_smem *smems, int64_t n, int32_t max_occ, int32_t mode,
+                      int64_t *coords, int64_t coords_cap, int32_t *counts, int64_t *total);
+/* The same over the last search of a read set, device-resident (the SMEMs in gb_fmi_results order,
+ * i.e. bwamem.cpp:737 for every read): sizes its buffers (one host sync), then expands and walks
+ * asynchronously on the read set's stream. */
+int gb_fmi_reads_sa_run(gb_fmi_reads *r, int32_t max_occ, int32_t mode);
+int gb_fmi_reads_sa_results(gb_fmi_reads *r, int64_t *coords, int64_t coords_cap, int32_t *counts,
+                            int64_t *total);
+/* Kernel time of the last SA run (row expansion + LF walks, HIP events), LF steps taken, coordinates. */
+int gb_fmi_reads_sa_timing(gb_fmi_reads *r, float *ms, int64_t *lf_steps, int64_t *coords);
 
 #ifdef __cplusplus
 }

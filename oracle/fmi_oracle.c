@@ -20,6 +20,9 @@
  *                 :1243-1326 (bwtSeedStrategyAllPosOneThread), :1499-1534 (compare_smem, sortSMEMs)
  *   batch driver  benchmarks/fmi/fmi.cpp:239-348 (smem1, reseed with split_len/splitWidth, LAST with
  *                 maxMemIntv=20 and minSeedLen+1, rid offset, per-batch sort)
+ *   SA lookup     FMI_search.cpp:1714-1807 (get_sa_entry_compressed: LF walk to a sampled row),
+ *                 :1834-1893 (call_one_step) and :1895-2040 (get_sa_entries_prefetch, the variant
+ *                 bwamem.cpp:737 calls), max_occ sampling of an SMEM's interval as in :1596-1619
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -49,6 +52,11 @@ typedef struct {
   int64_t cp_occ_size;
   uint64_t one_hot_mask[64];
   int64_t bwt_calls; /* backwardExt counter (work accounting for the roofline) */
+  int64_t sa_ns;     /* sampled SA (every 8th row): (n >> SA_COMPX) + 1 entries, or 0 */
+  int8_t *sa_ms_byte;
+  uint32_t *sa_ls_word;
+  int64_t lf_steps;  /* SA-lookup LF steps (work accounting) */
+  const int64_t *sa64; /* adopted packed samples (sa_ms_byte << 32 + sa_ls_word), or NULL */
 } or_fmi;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -144,28 +152,25 @@ int fmi_oracle_build(const uint8_t *ref, int64_t ref_len, const char *path, or_f
     }
     cc[bwt[i]]++;
   }
+  const int64_t ns = (n >> SA_COMPX) + 1;
+  int8_t *ms = (int8_t *)calloc((size_t)ns, 1);
+  uint32_t *ls = (uint32_t *)calloc((size_t)ns, 4);
+  for (int64_t i = 0, pos = 0; i < n; i++)
+    if ((i & ((1 << SA_COMPX) - 1)) == 0) {
+      ls[pos] = (uint32_t)(sa[i] & 0xffffffff);
+      ms[pos] = (int8_t)((sa[i] >> 32) & 0xff);
+      pos++;
+    }
   if (path) {
     FILE *fp = fopen(path, "wb");
     if (!fp) return -1;
     fwrite(&n, sizeof(int64_t), 1, fp);
     fwrite(count, sizeof(int64_t), 5, fp);
     fwrite(cp, sizeof(or_cp_occ), (size_t)cp_size, fp);
-    const int64_t ns = (n >> SA_COMPX) + 1;
-    int8_t *ms = (int8_t *)malloc((size_t)ns);
-    uint32_t *ls = (uint32_t *)malloc((size_t)ns * 4);
-    int64_t pos = 0;
-    for (int64_t i = 0; i < n; i++)
-      if ((i & ((1 << SA_COMPX) - 1)) == 0) {
-        ls[pos] = (uint32_t)(sa[i] & 0xffffffff);
-        ms[pos] = (int8_t)((sa[i] >> 32) & 0xff);
-        pos++;
-      }
     fwrite(ms, 1, (size_t)ns, fp);
     fwrite(ls, 4, (size_t)ns, fp);
     fwrite(&sentinel, sizeof(int64_t), 1, fp);
     fclose(fp);
-    free(ms);
-    free(ls);
   }
   if (idx) {
     idx->n = n;
@@ -177,8 +182,14 @@ int fmi_oracle_build(const uint8_t *ref, int64_t ref_len, const char *path, or_f
     idx->one_hot_mask[0] = 0;
     idx->one_hot_mask[1] = 0x8000000000000000ull;
     for (int i = 2; i < 64; i++) idx->one_hot_mask[i] = (idx->one_hot_mask[i - 1] >> 1) | 0x8000000000000000ull;
+    idx->sa_ns = ns;
+    idx->sa_ms_byte = ms;
+    idx->sa_ls_word = ls;
+    idx->lf_steps = 0;
   } else {
     free(cp);
+    free(ms);
+    free(ls);
   }
   free(bwt);
   free(sa);
@@ -196,7 +207,9 @@ int fmi_oracle_load(const char *path, or_fmi *idx) {
   or_cp_occ *cp = (or_cp_occ *)malloc((size_t)cp_size * sizeof(or_cp_occ));
   if (fread(cp, sizeof(or_cp_occ), (size_t)cp_size, fp) != (size_t)cp_size) return -3;
   const int64_t ns = (n >> SA_COMPX) + 1;
-  if (fseek(fp, ns * 5, SEEK_CUR)) return -4;
+  int8_t *ms = (int8_t *)malloc((size_t)ns);
+  uint32_t *ls = (uint32_t *)malloc((size_t)ns * 4);
+  if (fread(ms, 1, (size_t)ns, fp) != (size_t)ns || fread(ls, 4, (size_t)ns, fp) != (size_t)ns) return -4;
   int64_t sentinel;
   if (fread(&sentinel, 8, 1, fp) != 1) return -5;
   fclose(fp);
@@ -209,6 +222,10 @@ int fmi_oracle_load(const char *path, or_fmi *idx) {
   idx->one_hot_mask[0] = 0;
   idx->one_hot_mask[1] = 0x8000000000000000ull;
   for (int i = 2; i < 64; i++) idx->one_hot_mask[i] = (idx->one_hot_mask[i - 1] >> 1) | 0x8000000000000000ull;
+  idx->sa_ns = ns;
+  idx->sa_ms_byte = ms;
+  idx->sa_ls_word = ls;
+  idx->lf_steps = 0;
   return 0;
 }
 
@@ -227,9 +244,19 @@ void fmi_oracle_adopt(or_fmi *idx, int64_t n, const int64_t *count5_file, int64_
   for (int i = 2; i < 64; i++) idx->one_hot_mask[i] = (idx->one_hot_mask[i - 1] >> 1) | 0x8000000000000000ull;
 }
 
+/* Adopt packed sampled-SA entries produced elsewhere (caller keeps them alive). */
+void fmi_oracle_adopt_sa64(or_fmi *idx, int64_t ns, const int64_t *sa64) {
+  idx->sa_ns = ns;
+  idx->sa64 = sa64;
+}
+
 void fmi_oracle_free(or_fmi *idx) {
   free(idx->cp_occ);
+  free(idx->sa_ms_byte);
+  free(idx->sa_ls_word);
   idx->cp_occ = NULL;
+  idx->sa_ms_byte = NULL;
+  idx->sa_ls_word = NULL;
 }
 
 static inline int64_t get_occ(const or_fmi *f, int64_t pp, int c) {
@@ -524,6 +551,7 @@ or_fmi *fmi_oracle_share(const or_fmi *f) {
   or_fmi *g = (or_fmi *)malloc(sizeof(or_fmi));
   *g = *f;
   g->bwt_calls = 0;
+  g->lf_steps = 0;
   return g;
 }
 void fmi_oracle_unshare(or_fmi *g) { free(g); }
@@ -536,3 +564,58 @@ const void *fmi_oracle_cp_occ(const or_fmi *f, int64_t *size) {
   *size = f->cp_occ_size;
   return f->cp_occ;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* SA lookup                                                                                   */
+/* ------------------------------------------------------------------------------------------ */
+static inline int64_t sa_sample(const or_fmi *f, int64_t sp) {
+  if (f->sa64) return f->sa64[sp >> SA_COMPX];
+  int64_t e = f->sa_ms_byte[sp >> SA_COMPX];
+  return (e << 32) + f->sa_ls_word[sp >> SA_COMPX];
+}
+
+/* mode 0: get_sa_entry_compressed (FMI_search.cpp:1714-1807): walk LF from row pos until a sampled
+ * row (pos % 8 == 0) and add the number of steps; reaching the sentinel row ('$' in the BWT, no base
+ * bit in CP_OCC) returns the step count (SA[sentinel row] = 0).
+ * mode 1: call_one_step repeated as get_sa_entries_prefetch does (:1834-1893, :1965-2035): identical
+ * except that reaching the sentinel row yields 0 whatever the step count (:1865-1869). */
+int64_t fmi_oracle_sa_entry(or_fmi *f, int64_t pos, int mode) {
+  int64_t offset = 0, sp = pos;
+  while (sp & ((1 << SA_COMPX) - 1)) {
+    const int64_t occ_id = sp >> CP_SHIFT, y = CP_BLOCK - (sp & CP_MASK) - 1;
+    const uint64_t *oh = f->cp_occ[occ_id].one_hot_bwt_str;
+    int b = 4;
+    for (int c = 0; c < 4; c++)
+      if ((oh[c] >> y) & 1) {
+        b = c;
+        break;
+      }
+    if (b == 4) return mode ? 0 : offset;
+    sp = f->count[b] + get_occ(f, sp, b);
+    offset++;
+    f->lf_steps++;
+  }
+  return sa_sample(f, sp) + offset;
+}
+
+/* SA coordinates of every SMEM (FMI_search.cpp:1596-1619 / :1895-1931): for SMEM i, rows
+ * j = k, k+step, ... (j < k+s, at most max_occ of them), step = s > max_occ ? s / max_occ : 1;
+ * coords are concatenated in SMEM order, counts[i] = number for SMEM i. Returns the total. */
+int64_t fmi_oracle_sa_entries(or_fmi *f, const or_smem *smems, int64_t n, int32_t max_occ, int mode,
+                              int64_t *coords, int32_t *counts) {
+  int64_t tot = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t hi = smems[i].k + smems[i].s;
+    const int64_t step = smems[i].s > max_occ ? smems[i].s / max_occ : 1;
+    int32_t c = 0;
+    for (int64_t j = smems[i].k; j < hi && c < max_occ; j += step, c++) coords[tot + c] = fmi_oracle_sa_entry(f, j, mode);
+    if (counts) counts[i] = c;
+    tot += c;
+  }
+  return tot;
+}
+
+void fmi_oracle_sa_lookup(or_fmi *f, const int64_t *rows, int64_t n, int mode, int64_t *out) {
+  for (int64_t i = 0; i < n; i++) out[i] = fmi_oracle_sa_entry(f, rows[i], mode);
+}
+int64_t fmi_oracle_lf_steps(const or_fmi *f) { return f->lf_steps; }

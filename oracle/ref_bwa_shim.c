@@ -6,6 +6,8 @@
  *   index     bwa_idx_build (tools/bwa/bwtindex.c:256) -> .pac/.bwt; bwt_restore_bwt (bwt.c:443)
  *   SMEMs     mem_collect_intv (tools/bwa/bwamem.c:114-162) restated below over bwt_smem1
  *             (bwt.c:353) and bwt_seed_strategy1 (bwt.c:358), without the final sort.
+ *   SA        bwt_restore_sa (bwt.c:421) + bwt_sa (bwt.c:86): SA value of BWT rows, the same row
+ *             numbering as bwa-mem2's (cross-check of FMI_search.cpp:1714 get_sa_entry_compressed).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -23,6 +25,14 @@ int ref_bwa_build(const char *fasta, const char *prefix) {
 
 void *ref_bwa_load(const char *bwt_path) { return bwt_restore_bwt(bwt_path); }
 void ref_bwa_free(void *bwt) { bwt_destroy((bwt_t *)bwt); }
+
+/* SA[rows[i]] via bwa v1's own sampled suffix array (<prefix>.sa, interval 32). */
+int ref_bwa_sa(void *bwtp, const char *sa_path, const int64_t *rows, int64_t n, int64_t *out) {
+  bwt_t *bwt = (bwt_t *)bwtp;
+  if (!bwt->sa) bwt_restore_sa(sa_path, bwt);
+  for (int64_t i = 0; i < n; i++) out[i] = (int64_t)bwt_sa(bwt, (bwtint_t)rows[i]);
+  return 0;
+}
 
 /* mem_collect_intv with opt = {min_seed_len, split_factor 1.5, split_width 10, max_mem_intv 20}.
  * Out: k, l, s, m (start), n (end, inclusive) for every interval; returns count or -1 on overflow. */

@@ -26,9 +26,16 @@ def _decl(lib):
     lib.fmi_oracle_bwt_calls.restype = i64
     lib.fmi_oracle_info.argtypes = [vp, vp, vp, vp]
     lib.fmi_oracle_adopt.argtypes = [vp, i64, vp, i64, vp]
+    lib.fmi_oracle_adopt_sa64.argtypes = [vp, i64, vp]
     lib.fmi_oracle_share.argtypes = [vp]
     lib.fmi_oracle_share.restype = vp
     lib.fmi_oracle_unshare.argtypes = [vp]
+    lib.fmi_oracle_sa_lookup.argtypes = [vp, vp, i64, ctypes.c_int, vp]
+    lib.fmi_oracle_sa_lookup.restype = None
+    lib.fmi_oracle_sa_entries.argtypes = [vp, vp, i64, ctypes.c_int32, ctypes.c_int, vp, vp]
+    lib.fmi_oracle_sa_entries.restype = i64
+    lib.fmi_oracle_lf_steps.argtypes = [vp]
+    lib.fmi_oracle_lf_steps.restype = i64
 
 
 class OracleIndex:
@@ -38,11 +45,14 @@ class OracleIndex:
             _decl(self.lib)
             self.lib._fmi_decl = True
         self.h = self.lib.fmi_oracle_new()
-        if adopt is not None:  # (n, count5_after_load, sentinel, cp_occ int64[rows, 8])
-            n, count5, sentinel, occ = adopt
+        if adopt is not None:  # (n, count5_after_load, sentinel, cp_occ int64[rows, 8][, packed SA])
+            n, count5, sentinel, occ = adopt[:4]
             self._occ = np.ascontiguousarray(occ)
             c = np.array([x - 1 for x in count5], np.int64)
             self.lib.fmi_oracle_adopt(self.h, n, c.ctypes.data, sentinel, self._occ.ctypes.data)
+            if len(adopt) > 4:
+                self._sa = np.ascontiguousarray(adopt[4], np.int64)
+                self.lib.fmi_oracle_adopt_sa64(self.h, len(self._sa), self._sa.ctypes.data)
             self._adopted = True
             return
         if load_path is not None:
@@ -105,6 +115,50 @@ class OracleIndex:
     def bwt_calls(self):
         return self.lib.fmi_oracle_bwt_calls(self.h)
 
+    def sa_lookup(self, rows, mode=0):
+        """SA value of each BWT row: mode 0 get_sa_entry_compressed, mode 1 call_one_step chain."""
+        rows = np.ascontiguousarray(rows, np.int64)
+        out = np.zeros(len(rows), np.int64)
+        self.lib.fmi_oracle_sa_lookup(self.h, rows.ctypes.data, len(rows), mode, out.ctypes.data)
+        return out
+
+    def sa_entries(self, smems, max_occ=500, mode=1):
+        """get_sa_entries(_prefetch) over an SMEM array -> (coords, per-SMEM counts)."""
+        smems = np.ascontiguousarray(smems, SMEM_DTYPE)
+        cap = int(np.minimum(smems["s"], max_occ).sum()) if len(smems) else 0
+        coords = np.zeros(max(cap, 1), np.int64)
+        counts = np.zeros(max(len(smems), 1), np.int32)
+        tot = self.lib.fmi_oracle_sa_entries(self.h, smems.ctypes.data, len(smems), max_occ, mode,
+                                             coords.ctypes.data, counts.ctypes.data)
+        assert tot == cap
+        return coords[:tot], counts[:len(smems)]
+
+    def lf_steps(self):
+        return self.lib.fmi_oracle_lf_steps(self.h)
+
+    def sa_entries_threaded(self, smems, threads, max_occ=500, mode=1):
+        """sa_entries over `threads` OS threads (shared tables); returns (coordinates, LF steps)."""
+        from concurrent.futures import ThreadPoolExecutor
+        smems = np.ascontiguousarray(smems, SMEM_DTYPE)
+        parts = np.array_split(np.arange(len(smems)), threads)
+
+        def work(ix):
+            if len(ix) == 0:
+                return 0, 0
+            sub = np.ascontiguousarray(smems[ix[0]:ix[-1] + 1])
+            h = self.lib.fmi_oracle_share(self.h)
+            cap = int(np.minimum(np.maximum(sub["s"], 0), max_occ).sum())
+            coords = np.zeros(max(cap, 1), np.int64)
+            tot = self.lib.fmi_oracle_sa_entries(h, sub.ctypes.data, len(sub), max_occ, mode,
+                                                 coords.ctypes.data, None)
+            steps = self.lib.fmi_oracle_lf_steps(h)
+            self.lib.fmi_oracle_unshare(h)
+            return tot, steps
+
+        with ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(work, parts))
+        return sum(r[0] for r in res), sum(r[1] for r in res)
+
     def close(self):
         if self.h:
             if getattr(self, "_adopted", False):
@@ -126,7 +180,16 @@ def ref_bwa():
     lib.ref_bwa_free.argtypes = [vp]
     lib.ref_bwa_collect.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, i64]
     lib.ref_bwa_collect.restype = i64
+    lib.ref_bwa_sa.argtypes = [vp, ctypes.c_char_p, vp, i64, vp]
     return lib
+
+
+def bwa_sa(lib, bwt, sa_path, rows):
+    """bwa v1 bwt_sa (tools/bwa/bwt.c:86) over its own .sa file."""
+    rows = np.ascontiguousarray(rows, np.int64)
+    out = np.zeros(len(rows), np.int64)
+    assert lib.ref_bwa_sa(bwt, sa_path.encode(), rows.ctypes.data, len(rows), out.ctypes.data) == 0
+    return out
 
 
 def bwa_smems(lib, bwt, codes, lens, min_seed_len=19):

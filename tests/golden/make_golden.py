@@ -107,6 +107,49 @@ def fmi_golden():
     print("wrote fmi_golden.npz:", len(rid), "SMEMs for", len(lens), "reads")
 
 
+def sa_coords(sa, k, s, max_occ):
+    """get_sa_entries' row sampling (FMI_search.cpp:1596-1619) over a full SA array."""
+    out, cnt = [], []
+    for kk, ss in zip(k.tolist(), s.tolist()):
+        step = ss // max_occ if ss > max_occ else 1
+        rows = list(range(kk, kk + ss, step))[:max_occ]
+        out.extend(sa[rows].tolist())
+        cnt.append(len(rows))
+    return np.array(out, np.int64), np.array(cnt, np.int32)
+
+
+def fmi_sa_golden():
+    """fmi_sa_golden.npz: SA values from bwa v1's own suffix array (tools/bwa bwt_restore_sa + bwt_sa,
+    bwt.c:86/421) over the fmi_golden reference -- every row whose SA value is < 64 (the walks that can
+    meet the sentinel row) plus 20000 random rows -- and the SA coordinates of the golden SMEMs with
+    max_occ 500 and 2 (get_sa_entries' sampling, FMI_search.cpp:1596-1619). bwa v1 stores SA[0] = -1
+    for the '$' row; bwa-mem2 stores |text| (FMI_search.cpp:425), which is what is kept here."""
+    import tempfile
+    import fmi_util
+    lib = fmi_util.ref_bwa()
+    if lib is None:
+        raise SystemExit("oracle/_ref/libref_bwa.so missing: run `make -C oracle ref` first")
+    z = np.load(os.path.join(HERE, "fmi_golden.npz"))
+    ref = z["ref"]
+    n = 2 * len(ref) + 1
+    with tempfile.TemporaryDirectory() as d:
+        gen.write_fasta(d + "/ref.fa", ref)
+        assert lib.ref_bwa_build((d + "/ref.fa").encode(), (d + "/ref").encode()) == 0
+        bwt = lib.ref_bwa_load((d + "/ref.bwt").encode())
+        sa = fmi_util.bwa_sa(lib, bwt, d + "/ref.sa", np.arange(n, dtype=np.int64))
+        lib.ref_bwa_free(bwt)
+    assert sa[0] == -1
+    sa[0] = n - 1
+    assert (np.sort(sa) == np.arange(n)).all()
+    rng = np.random.default_rng(31)
+    rows = np.unique(np.concatenate([np.nonzero(sa < 64)[0], rng.integers(0, n, 20000)]))
+    c500, n500 = sa_coords(sa, z["k"], z["s"], 500)
+    c2, n2 = sa_coords(sa, z["k"], z["s"], 2)
+    np.savez_compressed(os.path.join(HERE, "fmi_sa_golden.npz"), rows=rows, sa=sa[rows],
+                        coords500=c500, counts500=n500, coords2=c2, counts2=n2)
+    print("wrote fmi_sa_golden.npz:", len(rows), "rows,", len(c500), "/", len(c2), "coordinates")
+
+
 def chain_inputs(seed=41):
     """Small call set exercising every branch of chain_dp: tiny calls, duplicate x (dr == 0),
     multi-segment calls (n_segs > 1, seg ids in y bits 48..55), mixed strands, long calls."""

@@ -74,3 +74,74 @@ def test_oracle_vs_bwa_live():
     oi = fmi_util.OracleIndex(ref)
     sm, _, _ = oi.run(codes, lens, batch_size=128)
     assert fmi_util.per_read(sm, len(lens)) == exp
+
+
+# ---------------------------------------------------------------- SA lookup (row f1 of SURVEY.md 8)
+
+@pytest.fixture(scope="module")
+def sa_golden():
+    return np.load(os.path.join(GOLDEN, "fmi_sa_golden.npz"))
+
+
+def golden_smems(z):
+    sm = np.zeros(len(z["k"]), fmi_util.SMEM_DTYPE)
+    for f in ("rid", "m", "n", "k", "l", "s"):
+        sm[f] = z[f]
+    return sm
+
+
+def test_sa_oracle_matches_bwa_golden(golden, sa_golden):
+    """get_sa_entry_compressed (FMI_search.cpp:1714) restated == bwa v1 bwt_sa on the same rows."""
+    oi = fmi_util.OracleIndex(golden["ref"])
+    assert (oi.sa_lookup(sa_golden["rows"], mode=0) == sa_golden["sa"]).all()
+    sm = golden_smems(golden)
+    for mo in (500, 2):
+        c, n = oi.sa_entries(sm, max_occ=mo, mode=0)
+        assert (n == sa_golden[f"counts{mo}"]).all()
+        assert (c == sa_golden[f"coords{mo}"]).all()
+    oi.close()
+
+
+def test_sa_prefetch_variant_sentinel_rule(golden, sa_golden):
+    """call_one_step (FMI_search.cpp:1834-1893) answers 0 where the walk meets the sentinel row after
+    >= 1 step; everywhere else it equals get_sa_entry_compressed. Those rows have SA < 64 here."""
+    oi = fmi_util.OracleIndex(golden["ref"])
+    rows, sa = sa_golden["rows"], sa_golden["sa"]
+    p = oi.sa_lookup(rows, mode=1)
+    diff = p != sa
+    assert diff.any() and (p[diff] == 0).all() and (sa[diff] > 0).all() and (sa[diff] < 64).all()
+    n, _, sent = oi.info()
+    # the row of SA value v < 64 walks v LF steps to the sentinel row unless it meets a sampled row first
+    assert (oi.sa_lookup([sent], mode=1) == 0).all() and (oi.sa_lookup([sent], mode=0) == 0).all()
+    oi.close()
+
+
+def test_sa_all_rows_permutation(tmp_path):
+    """Every row of a small index: mode 0 is a permutation of [0, n) and matches the file round trip."""
+    ref = gen.fmi_reference(20_000, seed=4, repeat_frac=0.2)
+    p = str(tmp_path / "s.bwt.2bit.64")
+    a = fmi_util.OracleIndex(ref, path_out=p)
+    b = fmi_util.OracleIndex(load_path=p)
+    n, _, _ = a.info()
+    rows = np.arange(n)
+    sa = a.sa_lookup(rows, 0)
+    assert (np.sort(sa) == rows).all()
+    assert (b.sa_lookup(rows, 0) == sa).all()
+    assert a.lf_steps() > 0
+
+
+def test_sa_oracle_vs_bwa_live(tmp_path):
+    lib = fmi_util.ref_bwa()
+    if lib is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    ref = gen.fmi_reference(60_000, seed=23, repeat_frac=0.3)
+    d = str(tmp_path)
+    gen.write_fasta(d + "/ref.fa", ref)
+    assert lib.ref_bwa_build((d + "/ref.fa").encode(), (d + "/ref").encode()) == 0
+    bwt = lib.ref_bwa_load((d + "/ref.bwt").encode())
+    n = 2 * len(ref) + 1
+    exp = fmi_util.bwa_sa(lib, bwt, d + "/ref.sa", np.arange(n))
+    lib.ref_bwa_free(bwt)
+    exp[0] = n - 1  # bwa v1 keeps -1 for the '$' row
+    oi = fmi_util.OracleIndex(ref)
+    assert (oi.sa_lookup(np.arange(n), 0) == exp).all()
