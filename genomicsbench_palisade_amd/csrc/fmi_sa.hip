@@ -298,7 +298,7 @@ int launch_walk(SaJob *J, gb_fmi_index *ix, int64_t n, int32_t mode) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, J->device) == hipSuccess) cus = prop.multiProcessorCount;
   const char *e = getenv("GB_SA_BLOCKS_PER_CU");
-  const int64_t per_cu = e ? std::max(1, atoi(e)) : 8;
+  const int64_t per_cu = e ? std::max(1, atoi(e)) : 4;  // 16 waves per CU: best of 2..16 (tools/sa_probe.py)
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cus * per_cu, (n + 255) / 256));
   hipLaunchKernelGGL(sa_walk, dim3((unsigned)blocks), dim3(256), 0, J->stream, A);
   GB_HIP(hipGetLastError());

@@ -13,7 +13,7 @@ import sys
 
 HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
        "smem_search": "smem_search", "chain_kernel": "chain_kernel", "bsw_extend_kernel": "bsw_extend_kernel",
-       "bsw_lane_kernel": "bsw_lane_kernel"}
+       "bsw_lane_kernel": "bsw_lane_kernel", "sa_walk": "sa_walk"}
 
 
 def name_of(r):
