@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -171,10 +172,15 @@ __device__ __forceinline__ float select_dist(uint32_t rmask, uint32_t h, float d
   uint32_t r = (m & __builtin_bit_cast(uint32_t, dmatch)) | (~m & __builtin_bit_cast(uint32_t, dmis));
   return __builtin_bit_cast(float, r);
 }
-// (f64: a plain select -- hipcc 7.2 mis-derives the high word of a sign-extended sbfe mask and
-// constant-folds it, so the 64-bit bit-insert form is not used.)
+// f64: the same mask applied to both halves. The mask comes from inline asm because hipcc 7.2
+// mis-derives the high word of a sign-extended sbfe mask and constant-folds it; asm is opaque.
 __device__ __forceinline__ double select_dist(uint32_t rmask, uint32_t h, double dmatch, double dmis) {
-  return ((rmask >> h) & 1u) ? dmatch : dmis;
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(rmask), "v"(h));
+  const uint64_t a = __builtin_bit_cast(uint64_t, dmatch), b = __builtin_bit_cast(uint64_t, dmis);
+  const uint32_t lo = (m & (uint32_t)a) | (~m & (uint32_t)b);
+  const uint32_t hi = (m & (uint32_t)(a >> 32)) | (~m & (uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
 // Per-lane constants of one stripe (initializeVectors, avx-pairhmm-template.h:83-128): the lane's
@@ -238,12 +244,17 @@ __device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const R
   const bool last_lane = lane == kWave - 1;
   constexpr int U = 4;
   int t = 0;
+  // The block's record reads and writes go through one VGPR address with immediate offsets (an
+  // SGPR base costs a v_mov per access); the asm zero keeps the compiler from rematerialising it.
+  int vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  Brec<T> *wb = bnd - (kWave - 2) + vzero;
   for (; t + U <= steps; t += U) {
     // records land directly in the DPP "old" registers (no rotation copies); the LDS latency is
     // covered by the other waves on the SIMD
-    const Brec<T> c0 = bnd[t + 1], c1 = bnd[t + 2], c2 = bnd[t + 3], c3 = bnd[t + 4];
+    Brec<T> *wr = wb + t;
+    const Brec<T> c0 = wr[kWave - 1], c1 = wr[kWave], c2 = wr[kWave + 1], c3 = wr[kWave + 2];
     const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
-    Brec<T> *wr = bnd + (t - (kWave - 2));
     phmm_step<T, kLast>(c0, h0, st, P, sumM, sumX, wr, last_lane);
     phmm_step<T, kLast>(c1, h1, st, P, sumM, sumX, wr + 1, last_lane);
     phmm_step<T, kLast>(c2, h2, st, P, sumM, sumX, wr + 2, last_lane);
@@ -609,17 +620,19 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipMemsetAsync(b->d_count, 0, sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
-    const size_t lds_f = (sizeof(Brec<float>) + 1) * (size_t)(b->max_haplen + kBndPad) + sizeof(Brec<float>) * kWave + kWave + 16;
-    const size_t lds_d = (sizeof(Brec<double>) + 1) * (size_t)(b->max_haplen + kBndPad) + sizeof(Brec<double>) * kWave + kWave + 16;
+    const size_t span = (size_t)(b->max_haplen + kBndPad + kWave);  // records and code bytes
+    const size_t lds_f = (sizeof(Brec<float>) + 1) * span + 16;
+    const size_t lds_d = (sizeof(Brec<double>) + 1) * span + 16;
+    auto f32k = phmm_forward<float, false>;
+    auto f64k = phmm_forward<double, true>;
     if (!b->force_f64) {
-      hipLaunchKernelGGL((phmm_forward<float, false>), dim3(n), dim3(kWave), lds_f, b->stream,
-                         b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,
-                         b->d_list, b->d_count);
+      hipLaunchKernelGGL(f32k, dim3(n), dim3(kWave), lds_f, b->stream, b->d_desc, b->d_pool,
+                         dev_tab<float>(t->f, t->hf.init_const), b->d_rf, b->d_list, b->d_count);
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
-    hipLaunchKernelGGL((phmm_forward<double, true>), dim3(n), dim3(kWave), lds_d, b->stream,
-                       b->d_desc, b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
+    hipLaunchKernelGGL(f64k, dim3(n), dim3(kWave), lds_d, b->stream, b->d_desc, b->d_pool,
+                       dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
                        b->force_f64 ? nullptr : b->d_list, b->force_f64 ? nullptr : b->d_count);
     GB_HIP(hipGetLastError());
     GB_HIP(hipEventRecord(b->ev[2], b->stream));
