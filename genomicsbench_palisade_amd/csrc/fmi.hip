@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -70,35 +71,34 @@ struct PList {  // one lane's view of its wave-interleaved scratch
 };
 
 struct DevIndex {
-  const Occ2 *occ;
+  const Occ32 *occ;
   int64_t count[5];
   int64_t sentinel;
 };
 
-__device__ __forceinline__ uint64_t occ_mask(int y) { return y ? (~0ull << (64 - y)) : 0ull; }
-
-// Occ(b, p) for b = A, C, G, T from one Occ2 line (GET_OCC, FMI_search.h:81-89, over the same
+// Occ(b, p) for b = A, C, G, T from one Occ32 block (GET_OCC, FMI_search.h:81-89, over the same
 // counts): T = p - A - C - G - [sentinel < p].
-__device__ __forceinline__ void occ4(const Occ2 &L, int64_t p, int64_t sentinel, int64_t o[4]) {
-  const int y = (int)(p & 127);
-  const uint64_t m0 = y >= 64 ? ~0ull : occ_mask(y), m1 = y > 64 ? occ_mask(y - 64) : 0ull;
-  const int64_t cA = (int64_t)(L.cnt[0] & ((1ull << 40) - 1));
-  const int64_t cC = (int64_t)((L.cnt[0] >> 40) | ((L.cnt[1] & 0xFFFFull) << 24));
-  const int64_t cG = (int64_t)(L.cnt[1] >> 16);
-  o[0] = cA + __popcll(L.a[0] & m0) + __popcll(L.a[1] & m1);
-  o[1] = cC + __popcll(L.c[0] & m0) + __popcll(L.c[1] & m1);
-  o[2] = cG + __popcll(L.g[0] & m0) + __popcll(L.g[1] & m1);
+__device__ __forceinline__ void occ4(const Occ32 &L, int64_t p, int64_t sentinel, int64_t o[4]) {
+  occ32_acg(L, p, o[0], o[1], o[2]);
   o[3] = p - o[0] - o[1] - o[2] - (sentinel < p ? 1 : 0);
 }
 
-// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). One 64-byte line covers
-// 128 rows; when sp and ep share a line the second load is skipped.
+// count[a] by selects over kernel-argument scalars: an indexed read would become a global load
+// issued after the Occ gather (a second dependent memory round trip per backwardExt)
+__device__ __forceinline__ int64_t count_of(const DevIndex &F, int a) {
+  return a == 0 ? F.count[0] : a == 1 ? F.count[1] : a == 2 ? F.count[2] : a == 3 ? F.count[3] : F.count[4];
+}
+
+// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). One 32-byte block covers
+// 64 rows; when sp and ep share a block the second load is skipped.
 __device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l, int64_t s, int a,
                                         int64_t &ko, int64_t &lo, int64_t &so) {
   const int64_t sp = k, ep = k + s;
-  const int64_t bs = sp >> 7, be = ep >> 7;
-  const Occ2 A = F.occ[bs];
-  Occ2 B;
+  const int64_t bs = sp >> 6, be = ep >> 6;
+  // the second line only when sp and ep fall in different lines (a duplicate request for the same
+  // line measured 10 % slower overall than the occasional wait for A)
+  const Occ32 A = F.occ[bs];
+  Occ32 B;
   if (be != bs)
     B = F.occ[be];
   else
@@ -109,12 +109,9 @@ __device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l,
   const int64_t off = (k <= F.sentinel && k + s > F.sentinel) ? 1 : 0;
   const int64_t s3 = oe[3] - os[3], s2 = oe[2] - os[2], s1 = oe[1] - os[1], s0 = oe[0] - os[0];
   const int64_t l3 = l + off, l2 = l3 + s3, l1 = l2 + s2, l0 = l1 + s1;
-  switch (a) {
-    case 0: ko = F.count[0] + os[0]; so = s0; lo = l0; break;
-    case 1: ko = F.count[1] + os[1]; so = s1; lo = l1; break;
-    case 2: ko = F.count[2] + os[2]; so = s2; lo = l2; break;
-    default: ko = F.count[3] + os[3]; so = s3; lo = l3; break;
-  }
+  ko = a == 0 ? F.count[0] + os[0] : a == 1 ? F.count[1] + os[1] : a == 2 ? F.count[2] + os[2] : F.count[3] + os[3];
+  so = a == 0 ? s0 : a == 1 ? s1 : a == 2 ? s2 : s3;
+  lo = a == 0 ? l0 : a == 1 ? l1 : a == 2 ? l2 : l3;
 }
 
 // byte codes -> 4-bit codes, 8 per word (base b of word w at bits 4*(b))
@@ -132,24 +129,27 @@ __global__ void pack_q4(const uint8_t *__restrict__ qdb, int32_t stride, int32_t
   q4[r * q4_stride + w] = v;
 }
 
-// CP_OCC (64 rows per line) -> Occ2 (128 rows per line)
-__global__ void compress_occ(const CpOcc *__restrict__ occ, int64_t cp_size, Occ2 *__restrict__ occ2,
-                             int64_t cp2_size) {
+// CP_OCC (one-hot planes, MSB = first row) -> Occ32 (2-bit codes, LSB = first row), one per block
+__global__ void compress_occ(const CpOcc *__restrict__ occ, int64_t cp_size, Occ32 *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cp2_size) return;
-  const CpOcc &b0 = occ[2 * i];
-  const bool has1 = 2 * i + 1 < cp_size;
-  Occ2 L;
-  L.a[0] = b0.one_hot_bwt_str[0];
-  L.c[0] = b0.one_hot_bwt_str[1];
-  L.g[0] = b0.one_hot_bwt_str[2];
-  L.a[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[0] : 0;
-  L.c[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[1] : 0;
-  L.g[1] = has1 ? occ[2 * i + 1].one_hot_bwt_str[2] : 0;
-  const uint64_t cA = (uint64_t)b0.cp_count[0], cC = (uint64_t)b0.cp_count[1], cG = (uint64_t)b0.cp_count[2];
-  L.cnt[0] = cA | (cC << 40);
-  L.cnt[1] = (cC >> 24) | (cG << 16);
-  occ2[i] = L;
+  if (i >= cp_size) return;
+  const CpOcc &b = occ[i];
+  uint64_t w[2] = {0, 0};
+  for (int r = 0; r < 64; r++) {
+    const int bit = 63 - r;
+    const uint64_t code = ((b.one_hot_bwt_str[0] >> bit) & 1)   ? 0
+                          : ((b.one_hot_bwt_str[1] >> bit) & 1) ? 1
+                          : ((b.one_hot_bwt_str[2] >> bit) & 1) ? 2
+                                                                 : 3;
+    w[r >> 5] |= code << (2 * (r & 31));
+  }
+  const uint64_t cA = (uint64_t)b.cp_count[0], cC = (uint64_t)b.cp_count[1], cG = (uint64_t)b.cp_count[2];
+  Occ32 L;
+  L.bwt[0] = w[0];
+  L.bwt[1] = w[1];
+  L.cnt[0] = cA | (cC << 34);
+  L.cnt[1] = (cC >> 30) | (cG << 4);
+  out[i] = L;
 }
 
 enum State : int {
@@ -188,7 +188,12 @@ struct SearchArgs {
   int32_t *ovf_n;
   int32_t *fatal;        // pass 2 overflow / list overflow
   unsigned long long *bwt_calls;
+  int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof
 };
+
+// Diagnostic phase clocks (GB_FMI_FLAGS & 4): per-wave s_memtime sums of [state machine, gather
+// wait, consume] and the trip count; read with gb_fmi_debug_prof().
+__device__ unsigned long long g_fmi_prof[4];
 
 __device__ __forceinline__ bool smem_less(const gb_smem &a, const gb_smem &b) {
   return a.m < b.m || (a.m == b.m && a.n > b.n);  // compare_smem, FMI_search.cpp:1499-1518
@@ -221,6 +226,7 @@ __device__ void heap_sort(gb_smem *a, int n) {
 // state machine are LDS reads instead of dependent global byte loads. Longer reads read d_qdb.
 constexpr int kQBases = 160;
 constexpr int kQW = kQBases / 8 + 1;  // words per lane row; odd, so same-word reads are conflict-free
+static_assert(kQBases % 32 == 0, "staging copies 32 bases per 16-byte load");
 
 template <bool kLdsQ>
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
@@ -229,10 +235,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   const int gid = blockIdx.x * 64 + threadIdx.x;
   PList prev;
   prev.base = A.scratch + (size_t)(gid >> 6) * A.stride * 64 + (gid & 63);
-  unsigned long long calls = 0, calls_read = 0;  // backwardExt calls (all reads / this read)
+  uint32_t calls = 0, calls_read = 0;  // backwardExt calls (all reads / this read)
 
   int st = NEXT_READ;
-  int rd = 0, L = 0, mode = 0;
+  int rd = 0, L = 0, mode = 0, nslot = -1;
   const uint8_t *q = nullptr;
   uint32_t *const qrow = Qs + (kLdsQ ? threadIdx.x * kQW : 0);
   auto base_at = [&](int idx) -> int {
@@ -249,7 +255,12 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   int64_t ck = 0, cl = 0, cs = 0;  // current SMEM of a forward extension
   uint32_t cm = 0;
   int r0 = 0;                      // reversed prev list: r[p] = prev[r0 + p] (r[0] = last pushed)
-  Ent cur{};                       // the prev entry of the pending BWD_P request
+  PEnt cur{};                      // the prev entry of the pending BWD_P request (packed)
+  // r[0] of the current list in registers, and r[p+1] loaded while r[p]'s backwardExt is in
+  // flight: the backward loop never waits on a scratch read before its gather. (Entries are
+  // compacted in place behind the read position, so a prefetched entry is never overwritten
+  // before it is used.)
+  PEnt head{};
 
   int cap = A.cap;  // slots of the current output area (kCap, or kBigCap once promoted)
   auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
@@ -279,7 +290,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     nout++;
   };
 
+  const bool prof = A.flags & 4;
+  unsigned long long p_sm = 0, p_mem = 0, p_cons = 0, p_trips = 0;
   while (true) {
+    const unsigned long long tA = prof ? clock64() : 0;
     // ---- advance this lane's state machine to its next backwardExt request --------------------
     int64_t rk = 0, rl = 0, rs = 0;
     int rb = 0;
@@ -287,17 +301,27 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     while (!req && st != DONE) {
       switch (st) {
         case NEXT_READ: {
-          const int slot = atomicAdd(A.next_read, 1);
+          // the slot of the following read is taken now and arrives while this read runs
+          const int slot = nslot >= 0 ? nslot : atomicAdd(A.next_read, 1);
           if (slot >= (A.list ? *A.list_n : A.nreads)) {
             st = DONE;
             break;
           }
+          nslot = atomicAdd(A.next_read, 1);
           rd = A.list ? A.list[slot] : slot;
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
           if constexpr (kLdsQ) {
-            const uint32_t *src = A.q4 + (size_t)rd * A.q4_stride;
-            for (int w = 0; w < ((L + 7) >> 3); w++) qrow[w] = src[w];
+            // rows are q4_stride (a multiple of 4) words: all 16-byte loads issue together
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.q4 + (size_t)rd * A.q4_stride);
+            const int n4 = (L + 31) >> 5;
+            for (int w = 0; w < n4; w++) {
+              const uint4 v = src[w];
+              qrow[4 * w] = v.x;
+              qrow[4 * w + 1] = v.y;
+              qrow[4 * w + 2] = v.z;
+              qrow[4 * w + 3] = v.w;
+            }
           }
           o = A.slots + (size_t)slot * A.cap;
           cap = A.cap;
@@ -324,9 +348,9 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             st = OP_END;
             break;
           }
-          ck = F.count[a];
-          cl = F.count[3 - a];
-          cs = F.count[a + 1] - F.count[a];
+          ck = count_of(F, a);
+          cl = count_of(F, 3 - a);
+          cs = count_of(F, a + 1) - ck;
           cm = (uint32_t)x;
           numPrev = 0;
           j = x + 1;
@@ -356,6 +380,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);  // current n = j-1
             prev.put(L - 1 - numPrev, e);
             numPrev++;
+            head = pack_ent(e);
           }
           r0 = L - numPrev;
           j = x - 1;
@@ -388,16 +413,19 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             }
             break;
           }
-          cur = prev.get(r0 + p);
-          rk = cur.k;
-          rl = cur.l;
-          rs = cur.s;
+          cur = p == 0 ? head : prev.base[(size_t)(r0 + p) * 64];
+          {
+            const Ent ce = unpack_ent(cur);
+            rk = ce.k;
+            rl = ce.l;
+            rs = ce.s;
+          }
           rb = a;
           req = true;
           break;
         case BWD_FINAL:
           if (numPrev != 0) {
-            const Ent e = prev.get(r0);
+            const Ent e = unpack_ent(head);  // r[0]
             if ((e.n - e.m + 1) >= (uint32_t)A.min_seed_len) emit(e.k, e.l, e.s, e.m, e.n);
           }
           st = OP_END;
@@ -447,9 +475,9 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             x = next_x;
             break;
           }
-          ck = F.count[a];
-          cl = F.count[3 - a];
-          cs = F.count[a + 1] - F.count[a];
+          ck = count_of(F, a);
+          cl = count_of(F, 3 - a);
+          cs = count_of(F, a + 1) - ck;
           cm = (uint32_t)x;
           j = x + 1;
           st = P3_NEXT;
@@ -474,20 +502,8 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           req = true;
           break;
         case FINISH: {
-          const int n = nout < cap ? nout : cap;
-          if (n <= 48) {
-            for (int i = 1; i < n; i++) {  // insertion sort by (m asc, n desc)
-              const gb_smem e = o[i];
-              int t = i - 1;
-              while (t >= 0 && smem_less(e, o[t])) {
-                o[t + 1] = o[t];
-                t--;
-              }
-              o[t + 1] = e;
-            }
-          } else {
-            heap_sort(o, n);  // promoted reads: O(n log n) (equal keys are identical SMEMs)
-          }
+          // the slot is sorted by (m asc, n desc) afterwards by sort_slots (an in-place sort here
+          // would be a chain of dependent global loads that stalls the whole wave)
           A.counts[rd] = nout;
           A.phase[3 * rd + 0] = n1;
           A.phase[3 * rd + 1] = n2;
@@ -506,8 +522,14 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
 
     // ---- one backwardExt per lane per trip --------------------------------------------------
     int64_t ko, lo, so;
+    const unsigned long long tB = prof ? clock64() : 0;
     bwt_ext(F, rk, rl, rs, rb, ko, lo, so);
     calls_read++;
+    unsigned long long tC = 0;
+    if (prof) {
+      asm volatile("" ::"v"(ko), "v"(lo), "v"(so));
+      tC = clock64();
+    }
 
     // ---- consume ------------------------------------------------------------------------------
     if (st == FWD_NEXT) {
@@ -518,6 +540,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);
         prev.put(L - 1 - numPrev, e);
         numPrev++;
+        head = pack_ent(e);
       }
       if (ns < min_intv) {
         next_x = j;
@@ -529,7 +552,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         j++;
       }
     } else if (st == BWD_P) {
-      const Ent e = cur;
+      const Ent e = unpack_ent(cur);
       if (first) {
         if (so < min_intv && (e.n - e.m + 1) >= (uint32_t)A.min_seed_len) {
           emit(e.k, e.l, e.s, e.m, e.n);
@@ -538,6 +561,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           curr_s = (int)so;
           Ent ne;
           ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
+          if (numCurr == 0) head = pack_ent(ne);  // r[0] of the next j
           prev.put(r0 + numCurr++, ne);
           first = false;
         }
@@ -545,6 +569,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         curr_s = (int)so;
         Ent ne;
         ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
+        if (numCurr == 0) head = pack_ent(ne);
         prev.put(r0 + numCurr++, ne);
       }
       p++;
@@ -560,8 +585,21 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         j++;
       }
     }
+    if (prof) {
+      const unsigned long long tD = clock64();
+      p_sm += tB - tA;
+      p_mem += tC - tB;
+      p_cons += tD - tC;
+      p_trips++;
+    }
   }
-  atomicAdd(A.bwt_calls, calls);
+  atomicAdd(A.bwt_calls, (unsigned long long)calls);
+  if (prof && (threadIdx.x & 63) == 0) {
+    atomicAdd(&g_fmi_prof[0], p_sm);
+    atomicAdd(&g_fmi_prof[1], p_mem);
+    atomicAdd(&g_fmi_prof[2], p_cons);
+    atomicAdd(&g_fmi_prof[3], p_trips);
+  }
 }
 
 // Reads with count <= kCap are in their pass-1 slot; the rest in the pass-2 slot at the position of
@@ -571,6 +609,38 @@ __global__ void mark_overflow(const int32_t *__restrict__ ovf_list, const int32_
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = min(*ovf_n, kMaxOvf);
   if (t < n) ovf_pos[ovf_list[t]] = t;
+}
+
+// Sort every read's slot by (m asc, n desc) (sortSMEMs / compare_smem, FMI_search.cpp:1499-1534),
+// one wave per read: lane i holds SMEM i and its rank comes from readlane broadcasts of the keys
+// (m < 2^13 and n < 2^13, checked on the host; equal keys are identical SMEMs). Promoted reads
+// (> kCap SMEMs) are heap-sorted by one lane.
+__global__ __launch_bounds__(256) void sort_slots(gb_smem *__restrict__ slots, gb_smem *__restrict__ big,
+                                                  const int32_t *__restrict__ ovf_pos,
+                                                  const int32_t *__restrict__ counts, int32_t nreads) {
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  for (int rd = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; rd < nreads; rd += nwaves) {
+    const int n = __builtin_amdgcn_readfirstlane(counts[rd]);
+    if (n <= 1) continue;
+    if (n <= kCap) {
+      gb_smem *src = slots + (size_t)rd * kCap;
+      gb_smem e{};
+      uint32_t key = 0xffffffffu;
+      if (lane < n) {
+        e = src[lane];
+        key = (e.m << 13) | (8191u - e.n);
+      }
+      int rank = 0;
+      for (int j = 0; j < n; j++) {
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, j);
+        rank += (kj < key || (kj == key && j < lane)) ? 1 : 0;
+      }
+      if (lane < n) src[rank] = e;
+    } else if (lane == 0) {
+      heap_sort(big + (size_t)ovf_pos[rd] * kBigCap, min(n, kBigCap));
+    }
+  }
 }
 
 __global__ void scatter_smems(const gb_smem *__restrict__ slots, const gb_smem *__restrict__ big,
@@ -636,12 +706,12 @@ int lanes_for_device() {
 
 namespace gbfmi {
 
-int ensure_occ2(gb_fmi_index *ix, hipStream_t s) {
-  if (ix->d_occ2) return GB_OK;
-  ix->cp2_size = (ix->n >> 7) + 1;
-  GB_HIP(hipMalloc(&ix->d_occ2, sizeof(Occ2) * (size_t)ix->cp2_size));
-  hipLaunchKernelGGL(compress_occ, dim3((unsigned)((ix->cp2_size + 255) / 256)), dim3(256), 0, s, ix->d_occ,
-                     ix->cp_size, ix->d_occ2, ix->cp2_size);
+int ensure_occ32(gb_fmi_index *ix, hipStream_t s) {
+  if (ix->d_occ32) return GB_OK;
+  GB_ARG(ix->n < (1ll << 34), "FM index too large for 34-bit Occ32 counts (%lld rows)", (long long)ix->n);
+  GB_HIP(hipMalloc(&ix->d_occ32, sizeof(Occ32) * (size_t)ix->cp_size));
+  hipLaunchKernelGGL(compress_occ, dim3((unsigned)((ix->cp_size + 255) / 256)), dim3(256), 0, s, ix->d_occ,
+                     ix->cp_size, ix->d_occ32);
   GB_HIP(hipGetLastError());
   GB_HIP(hipStreamSynchronize(s));  // other read sets of this index may use other streams
   return GB_OK;
@@ -708,6 +778,18 @@ int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n) {
 }  // namespace gbfmi
 
 extern "C" {
+
+int gb_fmi_debug_prof(uint64_t out[4], int reset) {
+  GB_ARG(out, "gb_fmi_debug_prof: null out");
+  GB_HIP(hipDeviceSynchronize());
+  GB_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(gbfmi::g_fmi_prof), sizeof(uint64_t) * 4));
+  if (reset) {
+    const uint64_t z[4] = {0, 0, 0, 0};
+    GB_HIP(hipMemcpyToSymbol(HIP_SYMBOL(gbfmi::g_fmi_prof), z, sizeof(z)));
+  }
+  return GB_OK;
+}
+
 
 int gb_fmi_index_load(const char *path, gb_fmi_index **out) {
   GB_ARG(path && out, "gb_fmi_index_load: null argument");
@@ -795,7 +877,7 @@ int gb_fmi_index_sa(gb_fmi_index *idx, int64_t *dst, int64_t dst_entries) {
 int gb_fmi_index_destroy(gb_fmi_index *idx) {
   if (!idx) return GB_OK;
   (void)hipFree(idx->d_occ);
-  (void)hipFree(idx->d_occ2);
+  (void)hipFree(idx->d_occ32);
   (void)hipFree(idx->d_sa);
   delete idx;
   return GB_OK;
@@ -836,7 +918,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
   if (e == hipSuccess) e = hipMalloc(&R->d_temp, std::max<size_t>(R->temp_bytes, 16));
   if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
-  R->q4_stride = (max_readlength + 7) / 8;
+  R->q4_stride = (((max_readlength + 7) / 8) + 3) & ~3;  // 16-byte rows (smem_search staging)
   if (e == hipSuccess) e = hipMalloc(&R->d_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
   if (e == hipSuccess && num_reads) {
     const int64_t nt = (int64_t)num_reads * R->q4_stride;
@@ -875,12 +957,12 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   GB_ARG(R, "gb_fmi_search: null read set");
   GB_ARG(min_seed_len > 0, "gb_fmi_search: min_seed_len %d", min_seed_len);
   GB_HIP(hipSetDevice(R->idx->device));
-  if (int st = gbfmi::ensure_occ2(R->idx, R->stream)) return st;
+  if (int st = gbfmi::ensure_occ32(R->idx, R->stream)) return st;
   GB_HIP(hipEventRecord(R->ev[0], R->stream));
   GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
   GB_HIP(hipMemsetAsync(R->d_calls, 0, 2 * sizeof(unsigned long long), R->stream));
   gbfmi::SearchArgs A;
-  A.F.occ = R->idx->d_occ2;
+  A.F.occ = R->idx->d_occ32;
   for (int b = 0; b < 5; b++) A.F.count[b] = R->idx->count[b];
   A.F.sentinel = R->idx->sentinel;
   A.qdb = R->d_qdb;
@@ -900,6 +982,10 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   A.ovf_n = R->d_ctl + 1;
   A.fatal = R->d_ctl + 2;
   A.bwt_calls = R->d_calls;
+  {
+    const char *e = getenv("GB_FMI_FLAGS");
+    A.flags = e ? atoi(e) : 0;
+  }
   if (R->nreads > 0) {
     // one pass: every read, kCap slots each; a read that outgrows them is promoted in place to a
     // kBigCap slot of the d_big pool
@@ -916,6 +1002,10 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     GB_HIP(hipGetLastError());
     hipLaunchKernelGGL(gbfmi::mark_overflow, dim3((gbfmi::kMaxOvf + 255) / 256), dim3(256), 0, R->stream,
                        R->d_ovf_list, R->d_ctl + 1, R->d_ovf_pos);
+    GB_HIP(hipGetLastError());
+    const int sort_blocks = std::max(1, std::min(256 * 8, (R->nreads + 3) / 4));
+    hipLaunchKernelGGL(gbfmi::sort_slots, dim3(sort_blocks), dim3(256), 0, R->stream, R->d_slots, R->d_big,
+                       R->d_ovf_pos, R->d_counts, R->nreads);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(R->ev[1], R->stream));

@@ -13,15 +13,41 @@ struct __attribute__((aligned(64))) CpOcc {
 };
 static_assert(sizeof(CpOcc) == 64, "CP_OCC is 64 bytes");
 
-// Search-side layout, one 64-byte line per 128 BWT rows (half the reference table): the A, C and G
-// one-hot planes of the two 64-row blocks (same bit order as CP_OCC) and the occurrence counts of
-// A, C, G before the line packed as three 40-bit fields. T is derived: rows before p minus A, C, G
-// minus the sentinel row (which carries no base bit).
-struct __attribute__((aligned(64))) Occ2 {
-  uint64_t a[2], c[2], g[2];
-  uint64_t cnt[2];  // cA | cC << 40, cC >> 24 | cG << 16
+// Search-side layout, one 32-byte block per 64 BWT rows (the same bytes per row as half a CP_OCC):
+// the 2-bit codes of rows [64b, 64b+64) (A0 C1 G2 T3, the sentinel row stored as 3; row r at bits
+// 2*(r & 31) of word r >> 5) and the A, C, G counts before the block as three 34-bit fields. A lane
+// reads one block with two 16-byte loads (a 64-byte line took four: the texture-address unit, which
+// walks the 64 scattered lane addresses of each load, is what bounds the gathers). T is derived:
+// rows before p minus A, C, G minus the sentinel row.
+struct __attribute__((aligned(32))) Occ32 {
+  uint64_t bwt[2];
+  uint64_t cnt[2];  // cA | cC << 34, cC >> 30 | cG << 4
 };
-static_assert(sizeof(Occ2) == 64, "Occ2 is 64 bytes");
+static_assert(sizeof(Occ32) == 32, "Occ32 is 32 bytes");
+
+constexpr uint64_t kEven = 0x5555555555555555ull;
+
+// A, C, G occurrences in rows [64b, p) of block b = p >> 6 plus the counts before the block.
+__device__ __forceinline__ void occ32_acg(const Occ32 &L, int64_t p, int64_t &oA, int64_t &oC, int64_t &oG) {
+  const int y = (int)(p & 63);
+  const int y0 = y < 32 ? y : 32, y1 = y > 32 ? y - 32 : 0;
+  const uint64_t m0 = y0 == 32 ? kEven : (((1ull << (2 * y0)) - 1) & kEven);
+  const uint64_t m1 = (((1ull << (2 * y1)) - 1) & kEven);  // y1 <= 31
+  const uint64_t lo0 = L.bwt[0] & kEven, hi0 = (L.bwt[0] >> 1) & kEven;
+  const uint64_t lo1 = L.bwt[1] & kEven, hi1 = (L.bwt[1] >> 1) & kEven;
+  const int64_t cA = (int64_t)(L.cnt[0] & ((1ull << 34) - 1));
+  const int64_t cC = (int64_t)((L.cnt[0] >> 34) | ((L.cnt[1] & 0xFull) << 30));
+  const int64_t cG = (int64_t)((L.cnt[1] >> 4) & ((1ull << 34) - 1));
+  oA = cA + __popcll(m0 & ~(lo0 | hi0)) + __popcll(m1 & ~(lo1 | hi1));
+  oC = cC + __popcll(m0 & lo0 & ~hi0) + __popcll(m1 & lo1 & ~hi1);
+  oG = cG + __popcll(m0 & hi0 & ~lo0) + __popcll(m1 & hi1 & ~lo1);
+}
+
+// 2-bit code of row p (3 for both T and the sentinel row).
+__device__ __forceinline__ int occ32_code(const Occ32 &L, int64_t p) {
+  const int y = (int)(p & 63);
+  return (int)((L.bwt[y >> 5] >> (2 * (y & 31))) & 3);
+}
 
 }  // namespace gbfmi
 
@@ -33,8 +59,7 @@ struct gb_fmi_index {
   int64_t sentinel = -1;
   int64_t cp_size = 0;      // (n >> 6) + 1 entries
   gbfmi::CpOcc *d_occ = nullptr;
-  int64_t cp2_size = 0;     // (n >> 7) + 1 lines
-  gbfmi::Occ2 *d_occ2 = nullptr;  // built from d_occ on first use
+  gbfmi::Occ32 *d_occ32 = nullptr;  // cp_size blocks, built from d_occ on first use
   int64_t sa_ns = 0;        // (n >> 3) + 1 sampled SA entries (SA_COMPX = 3, macro.h:64-66)
   int64_t *d_sa = nullptr;  // sa_ms_byte << 32 + sa_ls_word, one int64 per sampled row
 };
@@ -43,8 +68,8 @@ struct gb_fmi_reads;
 struct gb_smem;
 
 namespace gbfmi {
-// fmi.hip: the search-side Occ2 table (built once per index, on `s`).
-int ensure_occ2(gb_fmi_index *ix, hipStream_t s);
+// fmi.hip: the search-side Occ32 table (built once per index, on `s`).
+int ensure_occ32(gb_fmi_index *ix, hipStream_t s);
 // fmi.hip: the last search's SMEMs compacted on the device in (rid, m, n desc) order.
 int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n);
 hipStream_t reads_stream(gb_fmi_reads *R);

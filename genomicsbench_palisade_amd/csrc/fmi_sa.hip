@@ -11,7 +11,7 @@
 //                            (< k+s, at most max_occ), step = s > max_occ ? s / max_occ : 1
 //
 // MI355X design: every coordinate is an independent chain of dependent random 64-byte gathers (one
-// Occ2 line per LF step, ~8-14 steps) ended by one 8-byte sampled-SA gather -- pure HBM/Infinity-Cache
+// Occ32 block per LF step, ~8-14 steps) ended by one 8-byte sampled-SA gather -- pure HBM/Infinity-Cache
 // latency work with no arithmetic to speak of. The reference keeps 20 walks in flight per CPU thread
 // and prefetches; here every lane of every resident wave owns one walk and issues one gather per loop
 // trip, so ~500k gathers are in flight. Walk lengths are geometric, so a lane that finishes takes the
@@ -56,7 +56,7 @@ struct SaJob {
 };
 
 struct WalkArgs {
-  const Occ2 *occ;
+  const Occ32 *occ;
   const int64_t *sa;
   int64_t c0, c1, c2, c3;  // count[] after the load-time +1
   int64_t sentinel;
@@ -128,33 +128,16 @@ __global__ __launch_bounds__(256) void sa_walk(WalkArgs A) {
         A.out[t] = A.sa[sp >> 3] + off;
         busy = false;
       } else {
-        const Occ2 L = A.occ[sp >> 7];
-        const int y = (int)(sp & 127);
-        const int bit = 63 - (y & 63);
-        const bool h = y >= 64;
-        const uint64_t pa = h ? L.a[1] : L.a[0], pc = h ? L.c[1] : L.c[0], pg = h ? L.g[1] : L.g[0];
-        int b;
-        if ((pa >> bit) & 1)
-          b = 0;
-        else if ((pc >> bit) & 1)
-          b = 1;
-        else if ((pg >> bit) & 1)
-          b = 2;
-        else
-          b = sp == A.sentinel ? 4 : 3;
+        const Occ32 L = A.occ[sp >> 6];
+        int b = occ32_code(L, sp);
+        if (b == 3 && sp == A.sentinel) b = 4;
         if (b == 4) {
           A.out[t] = A.mode ? 0 : off;
           busy = false;
         } else {
           // Occ(b, sp): rows before sp carrying b (GET_OCC, FMI_search.h:81-89)
-          const uint64_t m0 = y >= 64 ? ~0ull : (y ? (~0ull << (64 - y)) : 0ull);
-          const uint64_t m1 = y > 64 ? (~0ull << (128 - y)) : 0ull;
-          const int64_t cA = (int64_t)(L.cnt[0] & ((1ull << 40) - 1));
-          const int64_t cC = (int64_t)((L.cnt[0] >> 40) | ((L.cnt[1] & 0xFFFFull) << 24));
-          const int64_t cG = (int64_t)(L.cnt[1] >> 16);
-          const int64_t oA = cA + __popcll(L.a[0] & m0) + __popcll(L.a[1] & m1);
-          const int64_t oC = cC + __popcll(L.c[0] & m0) + __popcll(L.c[1] & m1);
-          const int64_t oG = cG + __popcll(L.g[0] & m0) + __popcll(L.g[1] & m1);
+          int64_t oA, oC, oG;
+          occ32_acg(L, sp, oA, oC, oG);
           const int64_t oT = sp - oA - oC - oG - (A.sentinel < sp ? 1 : 0);
           sp = b == 0 ? A.c0 + oA : b == 1 ? A.c1 + oC : b == 2 ? A.c2 + oG : A.c3 + oT;
           off++;
@@ -282,7 +265,7 @@ int launch_walk(SaJob *J, gb_fmi_index *ix, int64_t n, int32_t mode) {
   GB_HIP(hipMemsetAsync(J->d_ctl, 0, 2 * sizeof(unsigned long long), J->stream));
   if (n == 0) return GB_OK;
   WalkArgs A;
-  A.occ = ix->d_occ2;
+  A.occ = ix->d_occ32;
   A.sa = ix->d_sa;
   A.c0 = ix->count[0];
   A.c1 = ix->count[1];
@@ -307,7 +290,7 @@ int launch_walk(SaJob *J, gb_fmi_index *ix, int64_t n, int32_t mode) {
 
 int check_index(gb_fmi_index *ix, hipStream_t s) {
   GB_ARG(ix->d_sa && ix->sa_ns == (ix->n >> 3) + 1, "SA lookup: index has no sampled suffix array");
-  return ensure_occ2(ix, s);
+  return ensure_occ32(ix, s);
 }
 
 int download(SaJob *J, int64_t *coords, int64_t coords_cap, int32_t *counts, int64_t *total) {

@@ -96,6 +96,10 @@ int gb_fmi_reads_sa_results(gb_fmi_reads *r, int64_t *coords, int64_t coords_cap
 /* Kernel time of the last SA run (row expansion + LF walks, HIP events), LF steps taken, coordinates. */
 int gb_fmi_reads_sa_timing(gb_fmi_reads *r, float *ms, int64_t *lf_steps, int64_t *coords);
 
+/* Diagnostic: per-wave clock sums of the search kernel's phases when GB_FMI_FLAGS has bit 2 (value
+ * 4) set -- out = {state machine, gather wait, consume, trips}; reset != 0 zeroes them. */
+int gb_fmi_debug_prof(uint64_t out[4], int reset);
+
 #ifdef __cplusplus
 }
 #endif
