@@ -193,7 +193,7 @@ struct SearchArgs {
 
 // Diagnostic phase clocks (GB_FMI_FLAGS & 4): per-wave s_memtime sums of [state machine, gather
 // wait, consume] and the trip count; read with gb_fmi_debug_prof().
-__device__ unsigned long long g_fmi_prof[4];
+__device__ unsigned long long g_fmi_prof[8];
 
 __device__ __forceinline__ bool smem_less(const gb_smem &a, const gb_smem &b) {
   return a.m < b.m || (a.m == b.m && a.n > b.n);  // compare_smem, FMI_search.cpp:1499-1518
@@ -291,14 +291,21 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   };
 
   const bool prof = A.flags & 4;
-  unsigned long long p_sm = 0, p_mem = 0, p_cons = 0, p_trips = 0;
+  unsigned long long p_sm = 0, p_mem = 0, p_cons = 0, p_trips = 0, p_iter = 0, p_nr_trips = 0, p_nr_clk = 0;
+  // next backwardExt request; `pend` = already prepared by the previous consume step (the common
+  // continuation of a forward, backward or LAST extension), which skips the state machine
+  int64_t rk = 0, rl = 0, rs = 0;
+  int rb = 0;
+  bool pend = false;
   while (true) {
     const unsigned long long tA = prof ? clock64() : 0;
     // ---- advance this lane's state machine to its next backwardExt request --------------------
-    int64_t rk = 0, rl = 0, rs = 0;
-    int rb = 0;
-    bool req = false;
+    bool req = pend;
+    pend = false;
+    bool took_read = false;
     while (!req && st != DONE) {
+      if (prof) p_iter++;
+      if (st == NEXT_READ) took_read = true;
       switch (st) {
         case NEXT_READ: {
           // the slot of the following read is taken now and arrives while this read runs
@@ -550,6 +557,18 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         cl = nl;
         cs = ns;
         j++;
+        if (j < L) {  // FWD_NEXT's request for the next base, inline
+          const int na = base_at(j);
+          if (na < 4) {
+            next_x = j + 1;
+            a = na;
+            rk = cl;
+            rl = ck;
+            rs = cs;
+            rb = 3 - na;
+            pend = true;
+          }
+        }
       }
     } else if (st == BWD_P) {
       const Ent e = unpack_ent(cur);
@@ -573,6 +592,15 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         prev.put(r0 + numCurr++, ne);
       }
       p++;
+      if (p < numPrev) {  // BWD_P's request for the next list entry, inline
+        cur = prev.base[(size_t)(r0 + p) * 64];
+        const Ent ce = unpack_ent(cur);
+        rk = ce.k;
+        rl = ce.l;
+        rs = ce.s;
+        rb = a;
+        pend = true;
+      }
     } else {  // P3_NEXT (bwtSeedStrategyAllPosOneThread)
       ck = lo;
       cl = ko;
@@ -583,6 +611,18 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         st = P3_X;
       } else {
         j++;
+        if (j < L) {  // P3_NEXT's request for the next base, inline
+          const int na = base_at(j);
+          if (na < 4) {
+            next_x = j + 1;
+            a = na;
+            rk = cl;
+            rl = ck;
+            rs = cs;
+            rb = 3 - na;
+            pend = true;
+          }
+        }
       }
     }
     if (prof) {
@@ -591,6 +631,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       p_mem += tC - tB;
       p_cons += tD - tC;
       p_trips++;
+      if (__ballot(took_read)) {
+        p_nr_trips++;
+        p_nr_clk += tB - tA;
+      }
     }
   }
   atomicAdd(A.bwt_calls, (unsigned long long)calls);
@@ -599,6 +643,12 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     atomicAdd(&g_fmi_prof[1], p_mem);
     atomicAdd(&g_fmi_prof[2], p_cons);
     atomicAdd(&g_fmi_prof[3], p_trips);
+    atomicAdd(&g_fmi_prof[5], p_nr_trips);
+    atomicAdd(&g_fmi_prof[6], p_nr_clk);
+  }
+  if (prof) {
+    // while-loop iterations: max over lanes per trip ~ wave iterations; sum of lane iterations here
+    atomicAdd(&g_fmi_prof[4], p_iter);
   }
 }
 
@@ -779,12 +829,12 @@ int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n) {
 
 extern "C" {
 
-int gb_fmi_debug_prof(uint64_t out[4], int reset) {
+int gb_fmi_debug_prof(uint64_t out[8], int reset) {
   GB_ARG(out, "gb_fmi_debug_prof: null out");
   GB_HIP(hipDeviceSynchronize());
-  GB_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(gbfmi::g_fmi_prof), sizeof(uint64_t) * 4));
+  GB_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(gbfmi::g_fmi_prof), sizeof(uint64_t) * 8));
   if (reset) {
-    const uint64_t z[4] = {0, 0, 0, 0};
+    const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     GB_HIP(hipMemcpyToSymbol(HIP_SYMBOL(gbfmi::g_fmi_prof), z, sizeof(z)));
   }
   return GB_OK;

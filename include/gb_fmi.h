@@ -97,8 +97,9 @@ int gb_fmi_reads_sa_results(gb_fmi_reads *r, int64_t *coords, int64_t coords_cap
 int gb_fmi_reads_sa_timing(gb_fmi_reads *r, float *ms, int64_t *lf_steps, int64_t *coords);
 
 /* Diagnostic: per-wave clock sums of the search kernel's phases when GB_FMI_FLAGS has bit 2 (value
- * 4) set -- out = {state machine, gather wait, consume, trips}; reset != 0 zeroes them. */
-int gb_fmi_debug_prof(uint64_t out[4], int reset);
+ * 4) set -- out = {state machine, gather wait, consume, trips, lane state-loop iterations, trips in
+ * which a lane took a new read, state-machine clocks of those trips, 0}; reset != 0 zeroes them. */
+int gb_fmi_debug_prof(uint64_t out[8], int reset);
 
 #ifdef __cplusplus
 }

@@ -21,9 +21,11 @@ for rep in range(2):
             import ctypes
             import numpy as np
             from genomicsbench_palisade_amd import lib
-            pr = np.zeros(4, np.uint64)
+            pr = np.zeros(8, np.uint64)
             lib().gb_fmi_debug_prof(ctypes.c_void_p(pr.ctypes.data), 1)
             tot = float(pr[:3].sum())
             extra = (f" | per wave-trip: state {pr[0] / pr[3]:.0f} gather {pr[1] / pr[3]:.0f} consume {pr[2] / pr[3]:.0f} clk"
-                     f" ({pr[0] / tot:.2f}/{pr[1] / tot:.2f}/{pr[2] / tot:.2f}), {int(pr[3])} wave-trips")
+                     f" ({pr[0] / tot:.2f}/{pr[1] / tot:.2f}/{pr[2] / tot:.2f}), {int(pr[3])} wave-trips;"
+                     f" lane state iters/lane-trip {pr[4] / pr[3] / 64:.2f}; new-read trips {pr[5] / pr[3]:.3f}"
+                     f" with state {pr[6] / max(pr[5], 1):.0f} clk (share of state time {pr[6] / pr[0]:.2f})")
         print(f"flags {fl}: search {a:.2f} ms total {b:.2f} ms, {calls / nreads:.1f} ext/read, {nreads / a / 1e3:.2f} Mreads/s{extra}", flush=True)
