@@ -301,8 +301,10 @@ def bench_chain(args, D, rank, world):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("chain: CPU baseline")
         cpu = cpu_baseline_chain(calls, args.cpu_seconds)
+    bt = bench_chain_backtrack(args, D, rank, world, b, calls)
     b.close()
     return {
+        "backtrack": bt,
         "value": round(manch, 3), "unit": "Manchors/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "config": {"workload": f"chain large: {calls.ncalls} calls, {calls.nanchors} anchors/rank (lognormal "
                                f"n, median 1500, max 87271), max_dist 5000, bw 500, n_segs 1",
@@ -311,6 +313,64 @@ def bench_chain(args, D, rank, world):
                      "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": pmc_traffic("chain_kernel"),
                      "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_kernel": ms},
+        "cpu_baseline": cpu,
+    }
+
+
+CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC = 3, 40  # minimap2 defaults (-n 3, -m 40)
+# algorithmic bytes per anchor of the backtrack: f, p, v read (12 B) + x, y of a chained anchor read
+# and written (32 B)
+CHAIN_BT_BYTES_PER_ANCHOR = 44
+
+
+def bench_chain_backtrack(args, D, rank, world, b, calls):
+    """Chain backtrack on the chain_dp outputs of the same batch: a step = one
+    backtrack pass over every call (the DP outputs stay resident on the device)."""
+    b.backtrack(CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC)
+    b.sync()
+    nch, _, nan, _, _, tc, ta = b.chains()
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    ks = []
+    for _ in range(args.steps):
+        b.backtrack(CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC)
+        b.sync()
+        ks.append(b.backtrack_timing())
+    device_sync()
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    manch = D.sum(float(calls.nanchors)) * args.steps / elapsed / 1e6
+    ms = float(np.mean(ks))
+    ach = CHAIN_BT_BYTES_PER_ANCHOR * calls.nanchors / (ms * 1e-3)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("chain backtrack: CPU baseline")
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        f, p, _, v, _ = b.results()
+        threads = min(16, _cores())
+        t1 = time.perf_counter()
+        reps = 0
+        while True:
+            oracle_lib.chain_bt_oracle(calls, f, p, v, CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC, threads)
+            reps += 1
+            if time.perf_counter() - t1 > min(args.cpu_seconds, 5.0):
+                break
+        dt = (time.perf_counter() - t1) / reps
+        cpu = {"value": calls.nanchors / dt / 1e6, "unit": "Manchors/s", "cores": threads, "kind": "port",
+               "sample": f"all {calls.ncalls} calls ({calls.nanchors} anchors) of the same set, C restatement of "
+                         f"the testbed backtrack (oracle/chain_oracle.c, pinned to mm_chain_dp), {reps} pass(es), "
+                         f"OpenMP {threads} threads"}
+    return {
+        "value": round(manch, 3), "unit": "Manchors/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": f"minimap2 chain backtrack (min_cnt {CHAIN_BT_MIN_CNT}, min_sc {CHAIN_BT_MIN_SC}) of "
+                               f"the chain_dp outputs of the same calls", "chains": int(tc),
+                   "chained_anchors": int(ta)},
+        "roofline": {"bound": "hbm", "kernel": "chain backtrack pipeline (k_first sweep dominant)",
+                     "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach / PEAK_HBM,
+                     "traffic": None, "bytes_per_anchor": CHAIN_BT_BYTES_PER_ANCHOR},
+        "kernels_ms": {"backtrack (all kernels of a step)": ms},
         "cpu_baseline": cpu,
     }
 

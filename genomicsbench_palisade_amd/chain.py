@@ -20,6 +20,9 @@ def _decl():
     L.gb_chain_batch_results.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gb_chain_batch_timing.argtypes = [vp, vp]
     L.gb_chain_batch_destroy.argtypes = [vp]
+    L.gb_chain_batch_backtrack.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+    L.gb_chain_batch_chains.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+    L.gb_chain_batch_backtrack_timing.argtypes = [vp, vp]
     L._chain_decl = True
     return L
 
@@ -50,6 +53,31 @@ class ChainBatch:
     def timing(self):
         ms = ctypes.c_float()
         check(_decl().gb_chain_batch_timing(self.h, ctypes.byref(ms)), "gb_chain_batch_timing")
+        return ms.value
+
+    def backtrack(self, min_cnt: int = 3, min_sc: int = 40):
+        """minimap2's chain backtrack on this batch's chain_dp outputs (asynchronous)."""
+        check(_decl().gb_chain_batch_backtrack(self.h, min_cnt, min_sc), "gb_chain_batch_backtrack")
+
+    def chains(self):
+        """-> (n_chains [ncalls], u [CSR at offsets], n_anchors [ncalls], ax, ay [CSR at 2*offsets],
+        total chains, total anchors)."""
+        c = self.calls
+        n = max(c.nanchors, 1)
+        nch = np.zeros(max(c.ncalls, 1), np.int64)
+        nan = np.zeros(max(c.ncalls, 1), np.int64)
+        u = np.zeros(n, np.uint64)
+        ax = np.zeros(2 * n, np.uint64)
+        ay = np.zeros(2 * n, np.uint64)
+        tc, ta = ctypes.c_int64(), ctypes.c_int64()
+        check(_decl().gb_chain_batch_chains(self.h, nch.ctypes.data, u.ctypes.data, nan.ctypes.data, ax.ctypes.data,
+                                            ay.ctypes.data, ctypes.byref(tc), ctypes.byref(ta)),
+              "gb_chain_batch_chains")
+        return nch[:c.ncalls], u, nan[:c.ncalls], ax, ay, tc.value, ta.value
+
+    def backtrack_timing(self):
+        ms = ctypes.c_float()
+        check(_decl().gb_chain_batch_backtrack_timing(self.h, ctypes.byref(ms)), "gb_chain_batch_backtrack_timing")
         return ms.value
 
     def close(self):

@@ -29,6 +29,7 @@
 
 #include "../../include/gb_chain.h"
 #include "gb_common.h"
+#include "chain_internal.h"
 
 namespace gbchain {
 
@@ -341,21 +342,6 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
 
 }  // namespace gbchain
 
-struct gb_chain_batch {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  int64_t ncalls = 0, nanchors = 0;
-  int64_t *d_off = nullptr;
-  float *d_aq = nullptr;
-  int32_t *d_par4 = nullptr, *d_order = nullptr;
-  uint64_t *d_x = nullptr, *d_y = nullptr;
-  int32_t *d_out = nullptr;  // score | parent | target | peak
-  unsigned long long *d_vis = nullptr;
-  unsigned long long *d_prof = nullptr;  // GB_CHAIN_PROF=1 phase clocks (development aid)
-  bool ran = false;
-};
-
 extern "C" {
 
 int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
@@ -483,6 +469,7 @@ int gb_chain_batch_timing(gb_chain_batch *B, float *kernel_ms) {
 int gb_chain_batch_destroy(gb_chain_batch *B) {
   if (!B) return GB_OK;
   if (B->stream) (void)hipStreamSynchronize(B->stream);
+  gbchain::chain_bt_destroy(B->bt);
   for (void *p : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order, (void *)B->d_x,
                   (void *)B->d_y, (void *)B->d_out, (void *)B->d_vis, (void *)B->d_prof})
     (void)hipFree(p);

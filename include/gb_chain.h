@@ -37,6 +37,21 @@ int gb_chain_batch_results(gb_chain_batch *b, int32_t *scores, int32_t *parents,
 int gb_chain_batch_timing(gb_chain_batch *b, float *kernel_ms);
 int gb_chain_batch_destroy(gb_chain_batch *b);
 
+/* Chain backtrack on the batch's chain_dp outputs (asynchronous): minimap2's consumer of score /
+ * parent / peak (tools/minimap2-acceleration/testbed/chain.c:140-219 == tools/minimap2/chain.c):
+ * chain ends -> peaks, ordered by score, claimed greedily, kept if >= min_cnt anchors and (when
+ * stopped by an earlier chain) score gain >= min_sc, reordered by the x of their first anchor.
+ * minimap2's defaults are min_cnt 3, min_sc 40. */
+int gb_chain_batch_backtrack(gb_chain_batch *b, int32_t min_cnt, int32_t min_sc);
+/* Results of the last backtrack (synchronous), CSR by the batch's offsets: call c's chains
+ * (score << 32 | anchor count, mm_chain_dp's u[]) at u[offsets[c] .. + n_chains[c]) and their anchors
+ * concatenated in chain order at ax/ay[2*offsets[c] .. + n_anchors[c]) (capacity 2n per call: a
+ * start that an earlier chain owns can be kept again as a one-anchor chain when min_cnt <= 1).
+ * Any output may be NULL; totals are over all calls. */
+int gb_chain_batch_chains(gb_chain_batch *b, int64_t *n_chains, uint64_t *u, int64_t *n_anchors,
+                          uint64_t *ax, uint64_t *ay, int64_t *total_chains, int64_t *total_anchors);
+int gb_chain_batch_backtrack_timing(gb_chain_batch *b, float *ms);
+
 /* One-shot form of host_chain_kernel over CSR arrays. */
 int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
              const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents,

@@ -104,3 +104,168 @@ int64_t chain_oracle_batch(int64_t ncalls, const int64_t *offsets, const float *
   }
   return total;
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * Chain backtrack: the consumer of chain_dp's score f[], parent p[] and peak v[] arrays in minimap2
+ * (tools/minimap2-acceleration/testbed/chain.c:140-219, the same code follows the DP in
+ * tools/minimap2/chain.c): chain ends -> their peaks, sorted by (score, index) descending, claimed
+ * greedily along parent links, then reordered by the x of each chain's first anchor. The two sorts
+ * are ksort.h's in-place MSD radix sort (KRADIX_SORT_INIT, ksort.h:93-150; 8 bits per pass,
+ * insertion sort below 64 elements), restated here because its order of equal keys is part of the
+ * output.
+ * --------------------------------------------------------------------------------------------- */
+typedef struct { uint64_t x, y; } bt128_t;
+
+#define BT_RS_MIN 64
+#define BT_RS_BITS 8
+
+#define BT_RADIX(name, T, KEY)                                                                       \
+  static void rs_ins_##name(T *beg, T *end) {                                                        \
+    for (T *i = beg + 1; i < end; ++i)                                                                \
+      if (KEY(*i) < KEY(*(i - 1))) {                                                                  \
+        T *j, tmp = *i;                                                                               \
+        for (j = i; j > beg && KEY(tmp) < KEY(*(j - 1)); --j) *j = *(j - 1);                          \
+        *j = tmp;                                                                                     \
+      }                                                                                               \
+  }                                                                                                   \
+  static void rs_sort_##name(T *beg, T *end, int n_bits, int s) {                                     \
+    const int size = 1 << n_bits, m = size - 1;                                                       \
+    struct { T *b, *e; } b[1 << BT_RS_BITS], *k, *be = b + size;                                      \
+    for (k = b; k != be; ++k) k->b = k->e = beg;                                                      \
+    for (T *i = beg; i != end; ++i) ++b[KEY(*i) >> s & m].e;                                          \
+    for (k = b + 1; k != be; ++k) k->e += (k - 1)->e - beg, k->b = (k - 1)->e;                       \
+    for (k = b; k != be;) {                                                                           \
+      if (k->b != k->e) {                                                                             \
+        __typeof__(b[0]) *l;                                                                          \
+        if ((l = b + (KEY(*k->b) >> s & m)) != k) {                                                   \
+          T tmp = *k->b, swap;                                                                        \
+          do {                                                                                        \
+            swap = tmp;                                                                               \
+            tmp = *l->b;                                                                              \
+            *l->b++ = swap;                                                                           \
+            l = b + (KEY(tmp) >> s & m);                                                              \
+          } while (l != k);                                                                           \
+          *k->b++ = tmp;                                                                              \
+        } else                                                                                        \
+          ++k->b;                                                                                     \
+      } else                                                                                          \
+        ++k;                                                                                          \
+    }                                                                                                 \
+    for (b->b = beg, k = b + 1; k != be; ++k) k->b = (k - 1)->e;                                      \
+    if (s) {                                                                                          \
+      s = s > n_bits ? s - n_bits : 0;                                                                \
+      for (k = b; k != be; ++k)                                                                       \
+        if (k->e - k->b > BT_RS_MIN)                                                                  \
+          rs_sort_##name(k->b, k->e, n_bits, s);                                                      \
+        else if (k->e - k->b > 1)                                                                     \
+          rs_ins_##name(k->b, k->e);                                                                  \
+    }                                                                                                 \
+  }                                                                                                   \
+  void bt_radix_sort_##name(T *beg, T *end) {                                                         \
+    if (end - beg <= BT_RS_MIN)                                                                       \
+      rs_ins_##name(beg, end);                                                                        \
+    else                                                                                              \
+      rs_sort_##name(beg, end, BT_RS_BITS, (8 - 1) * BT_RS_BITS);                                     \
+  }
+
+#define BT_KEY64(a) (a)
+#define BT_KEY128(a) ((a).x)
+BT_RADIX(64, uint64_t, BT_KEY64)
+BT_RADIX(128x, bt128_t, BT_KEY128)
+
+/* One call (testbed/chain.c:140-219). u_out gets the chains (score << 32 | anchor count) in output
+ * order, bx/by their anchors concatenated (capacity 2n: a chain start that an earlier chain already
+ * claimed can be emitted again as a one-anchor chain when min_cnt <= 1). Returns the chain count;
+ * *n_anchors = anchors written. */
+int64_t chain_oracle_backtrack(int64_t n, const int32_t *f, const int32_t *p, const int32_t *v,
+                               const uint64_t *ax, const uint64_t *ay, int min_cnt, int min_sc,
+                               uint64_t *u_out, uint64_t *bx, uint64_t *by, int64_t *n_anchors) {
+  *n_anchors = 0;
+  if (n <= 0) return 0;
+  int32_t *t = (int32_t *)calloc((size_t)n, 4), *vv = (int32_t *)malloc((size_t)n * 8);
+  int64_t i, j, n_u, n_v, k;
+  for (i = 0; i < n; ++i)
+    if (p[i] >= 0) t[p[i]] = 1;
+  for (i = n_u = 0; i < n; ++i)
+    if (t[i] == 0 && v[i] >= min_sc) ++n_u;
+  if (n_u == 0) {
+    free(t);
+    free(vv);
+    return 0;
+  }
+  uint64_t *u = (uint64_t *)malloc((size_t)n_u * 8);
+  for (i = n_u = 0; i < n; ++i) {
+    if (t[i] == 0 && v[i] >= min_sc) {
+      j = i;
+      while (j >= 0 && f[j] < v[j]) j = p[j];  // the peak that maximizes f[]
+      if (j < 0) j = i;
+      u[n_u++] = (uint64_t)f[j] << 32 | (uint64_t)j;
+    }
+  }
+  bt_radix_sort_64(u, u + n_u);
+  for (i = 0; i < n_u >> 1; ++i) {  // highest score first
+    const uint64_t tmp = u[i];
+    u[i] = u[n_u - i - 1], u[n_u - i - 1] = tmp;
+  }
+  for (i = 0; i < n; ++i) t[i] = 0;
+  for (i = n_v = k = 0; i < n_u; ++i) {
+    const int64_t n_v0 = n_v, k0 = k;
+    j = (int32_t)u[i];
+    do {
+      vv[n_v++] = (int32_t)j;
+      t[j] = 1;
+      j = p[j];
+    } while (j >= 0 && t[j] == 0);
+    if (j < 0) {
+      if (n_v - n_v0 >= min_cnt) u[k++] = u[i] >> 32 << 32 | (uint64_t)(n_v - n_v0);
+    } else if ((int32_t)(u[i] >> 32) - f[j] >= min_sc) {
+      if (n_v - n_v0 >= min_cnt) u[k++] = ((u[i] >> 32) - (uint64_t)f[j]) << 32 | (uint64_t)(n_v - n_v0);
+    }
+    if (k0 == k) n_v = n_v0;
+  }
+  n_u = k;
+  bt128_t *b = (bt128_t *)malloc((size_t)(n_v > 0 ? n_v : 1) * sizeof(bt128_t));
+  for (i = 0, k = 0; i < n_u; ++i) {
+    const int64_t k0 = k, ni = (int32_t)u[i];
+    for (j = 0; j < ni; ++j) {
+      const int32_t a = vv[k0 + (ni - j - 1)];
+      b[k].x = ax[a], b[k].y = ay[a], ++k;
+    }
+  }
+  bt128_t *w = (bt128_t *)malloc((size_t)n_u * sizeof(bt128_t));
+  for (i = k = 0; i < n_u; ++i) {
+    w[i].x = b[k].x, w[i].y = (uint64_t)k << 32 | (uint64_t)i;
+    k += (int32_t)u[i];
+  }
+  bt_radix_sort_128x(w, w + n_u);
+  for (i = k = 0; i < n_u; ++i) {
+    const int64_t jj = (int32_t)w[i].y, nn = (int32_t)u[jj];
+    u_out[i] = u[jj];
+    for (int64_t q = 0; q < nn; q++) {
+      bx[k + q] = b[(w[i].y >> 32) + q].x;
+      by[k + q] = b[(w[i].y >> 32) + q].y;
+    }
+    k += nn;
+  }
+  *n_anchors = k;
+  free(t);
+  free(vv);
+  free(u);
+  free(b);
+  free(w);
+  return n_u;
+}
+
+/* All calls (CSR): u_out[offsets[c] ..) and bx/by[2*offsets[c] ..) per call; n_chains[c],
+ * n_anchor[c] counts. OpenMP over calls. */
+void chain_oracle_backtrack_batch(int64_t ncalls, const int64_t *offsets, const int32_t *f, const int32_t *p,
+                                  const int32_t *v, const uint64_t *ax, const uint64_t *ay, int min_cnt,
+                                  int min_sc, uint64_t *u_out, uint64_t *bx, uint64_t *by, int64_t *n_chains,
+                                  int64_t *n_anchor, int nthreads) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int64_t c = 0; c < ncalls; c++) {
+    const int64_t o = offsets[c], n = offsets[c + 1] - o;
+    n_chains[c] = chain_oracle_backtrack(n, f + o, p + o, v + o, ax + o, ay + o, min_cnt, min_sc, u_out + o,
+                                         bx + 2 * o, by + 2 * o, n_anchor + c);
+  }
+}

@@ -195,6 +195,65 @@ def chain_golden():
     print("wrote chain_golden.npz:", c.ncalls, "calls,", c.nanchors, "anchors")
 
 
+CHAIN_BT_PARAMS = [(3, 40), (1, 0), (2, 15)]  # (min_cnt, min_sc): minimap2 defaults, everything, between
+
+
+def chain_bt_inputs(seed=43):
+    """Single-segment calls (the testbed asserts sidi == sidj) with avg_qspan computed as the
+    testbed does from the anchors ((float)sum_qspan / n, testbed/chain.c:40-41): generator calls,
+    n = 1 and 2, a call with long duplicate-x runs (ties in the final reorder) and a long call."""
+    rng = np.random.default_rng(seed)
+    calls = gen.chain_dataset("small", num_calls=60, seed=seed, median_n=300, max_n=6000)
+    offs, xs, ys = [0], [], []
+    for c in range(calls.ncalls):
+        o0, o1 = calls.offsets[c], calls.offsets[c + 1]
+        xs.append(calls.x[o0:o1]); ys.append(calls.y[o0:o1]); offs.append(offs[-1] + (o1 - o0))
+    extra = [(np.array([5000], np.uint64), np.array([(15 << 32) | 100], np.uint64)),
+             (np.array([5000, 5010], np.uint64), np.array([(15 << 32) | 100, (15 << 32) | 110], np.uint64))]
+    n = 1500
+    x = np.sort(rng.integers(10_000, 14_000, n)).astype(np.uint64)
+    x[200:260] = x[200]
+    q = rng.integers(0, 4000, n).astype(np.uint64)
+    y = (np.uint64(19) << np.uint64(32)) | q
+    o = np.lexsort((y, x))
+    extra.append((x[o], y[o]))
+    x2, y2, _ = gen.chain_call(rng, 8000)
+    extra.append((x2, y2))
+    for x, y in extra:
+        xs.append(np.asarray(x, np.uint64)); ys.append(np.asarray(y, np.uint64)); offs.append(offs[-1] + len(x))
+    offs = np.array(offs)
+    x, y = np.concatenate(xs), np.concatenate(ys)
+    aq = []
+    for c in range(len(offs) - 1):
+        span = ((y[offs[c]:offs[c + 1]] >> np.uint64(32)) & np.uint64(0xff)).sum()
+        aq.append(np.float32(int(span)) / np.float32(offs[c + 1] - offs[c]))
+    nc = len(offs) - 1
+    return gen.ChainCalls(offs, x, y, np.array(aq, np.float32), np.tile(np.array([5000, 5000, 500, 1], np.int32), (nc, 1)))
+
+
+def chain_bt_golden():
+    """chain_bt_golden.npz: chains of the reference minimap2-acceleration testbed mm_chain_dp (DP +
+    backtrack + reorder, oracle/_ref/libref_chain_bt.so) for chain_bt_inputs(), per CHAIN_BT_PARAMS
+    set k: u{k} (chains of all calls concatenated), nch{k} (chains per call), bx{k}/by{k} (anchors
+    concatenated), nan{k} (anchors per call)."""
+    lib = oracle_lib.ref_chain_bt()
+    if lib is None:
+        raise SystemExit("oracle/_ref/libref_chain_bt.so missing: run `make -C oracle ref` first")
+    c = chain_bt_inputs()
+    arrs = dict(offsets=c.offsets, x=c.x, y=c.y, avg_qspan=c.avg_qspan, params4=c.params4,
+                bt_params=np.array(CHAIN_BT_PARAMS, np.int32))
+    for k, (mc, ms) in enumerate(CHAIN_BT_PARAMS):
+        us, an = oracle_lib.ref_chain_bt_run(lib, c, mc, ms)
+        arrs[f"u{k}"] = np.concatenate(us) if us else np.zeros(0, np.uint64)
+        arrs[f"nch{k}"] = np.array([len(u) for u in us], np.int64)
+        arrs[f"bx{k}"] = np.concatenate([a[0] for a in an])
+        arrs[f"by{k}"] = np.concatenate([a[1] for a in an])
+        arrs[f"nan{k}"] = np.array([len(a[0]) for a in an], np.int64)
+    np.savez_compressed(os.path.join(HERE, "chain_bt_golden.npz"), **arrs)
+    print("wrote chain_bt_golden.npz:", c.ncalls, "calls,", c.nanchors, "anchors,",
+          [int(arrs[f"nch{k}"].sum()) for k in range(len(CHAIN_BT_PARAMS))], "chains")
+
+
 def bsw_inputs(seed=77):
     """Synthetic pairs shaped like the bsw datasets plus edge pairs: qlen 1 and 255 (the buffer
     maximum), tlen 1, a target much longer than query + w (empty bands), all-N sequences, identical
@@ -248,6 +307,7 @@ def bsw_golden():
 def main():
     bsw_golden()
     chain_golden()
+    chain_bt_golden()
     fmi_golden()
     ref = oracle_lib.ref_phmm()
     if ref is None:

@@ -133,3 +133,74 @@ def ref_bsw_run(lib, pairs, params):
     keep, a = _bsw_args(pairs, params)
     lib.ref_bwa_ksw_batch(*a, out.ctypes.data)
     return out[:pairs.n]
+
+
+def chain_bt_oracle(calls, f, p, v, min_cnt=3, min_sc=40, nthreads=4):
+    """oracle/chain_oracle.c chain_oracle_backtrack_batch -> (n_chains [ncalls], u list, (bx, by) list)
+    per call, from chain_dp outputs f (scores), p (parents), v (peak scores)."""
+    import numpy as np
+    lib = oracle()
+    if not getattr(lib, "_chain_bt_decl", False):
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.chain_oracle_backtrack_batch.argtypes = [i64, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int,
+                                                     vp, vp, vp, vp, vp, ctypes.c_int]
+        lib.chain_oracle_backtrack_batch.restype = None
+        lib._chain_bt_decl = True
+    n = max(calls.nanchors, 1)
+    f, p, v = (np.ascontiguousarray(a, np.int32) for a in (f, p, v))
+    u = np.zeros(n, np.uint64)
+    bx = np.zeros(2 * n, np.uint64)
+    by = np.zeros(2 * n, np.uint64)
+    nch = np.zeros(max(calls.ncalls, 1), np.int64)
+    nan = np.zeros(max(calls.ncalls, 1), np.int64)
+    lib.chain_oracle_backtrack_batch(calls.ncalls, calls.offsets.ctypes.data, f.ctypes.data, p.ctypes.data,
+                                     v.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data, min_cnt, min_sc,
+                                     u.ctypes.data, bx.ctypes.data, by.ctypes.data, nch.ctypes.data,
+                                     nan.ctypes.data, nthreads)
+    return unpack_chain_bt(calls.offsets, calls.ncalls, nch, nan, u, bx, by)
+
+
+def unpack_chain_bt(offsets, ncalls, nch, nan, u, bx, by):
+    """CSR backtrack outputs (u at offsets[c], anchors at 2*offsets[c]) -> per-call lists."""
+    us, anchors = [], []
+    for c in range(ncalls):
+        o = int(offsets[c])
+        us.append(u[o:o + int(nch[c])].copy())
+        anchors.append((bx[2 * o:2 * o + int(nan[c])].copy(), by[2 * o:2 * o + int(nan[c])].copy()))
+    return nch[:ncalls].copy(), us, anchors
+
+
+def ref_chain_bt():
+    """The minimap2-acceleration testbed mm_chain_dp (DP + backtrack) compiled from the reference
+    tree (oracle/_ref/libref_chain_bt.so) or None."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libref_chain_bt.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    lib.ref_chain_dp_bt.argtypes = [i64, ci, ci, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp]
+    lib.ref_chain_dp_bt.restype = i64
+    return lib
+
+
+def ref_chain_bt_run(lib, calls, min_cnt=3, min_sc=40, max_skip=25):
+    """Per call: (u, (bx, by)) from the reference mm_chain_dp. The reference computes avg_qspan from
+    the anchors (testbed/chain.c:40-41); callers compare on calls whose avg_qspan field equals that."""
+    import numpy as np
+    us, anchors = [], []
+    for c in range(calls.ncalls):
+        o0, o1 = int(calls.offsets[c]), int(calls.offsets[c + 1])
+        n = o1 - o0
+        x = np.ascontiguousarray(calls.x[o0:o1])
+        y = np.ascontiguousarray(calls.y[o0:o1])
+        u = np.zeros(max(n, 1), np.uint64)
+        bx = np.zeros(2 * max(n, 1), np.uint64)
+        by = np.zeros(2 * max(n, 1), np.uint64)
+        na = ctypes.c_int64()
+        p4 = np.asarray(calls.params4).reshape(-1)[4 * c:4 * c + 4]
+        k = lib.ref_chain_dp_bt(n, int(p4[0]), int(p4[1]), int(p4[2]), max_skip, min_cnt, min_sc, int(p4[3]),
+                                x.ctypes.data, y.ctypes.data, u.ctypes.data, bx.ctypes.data, by.ctypes.data,
+                                ctypes.byref(na))
+        us.append(u[:k].copy())
+        anchors.append((bx[:na.value].copy(), by[:na.value].copy()))
+    return us, anchors
