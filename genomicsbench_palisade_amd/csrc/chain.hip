@@ -124,83 +124,97 @@ __device__ __forceinline__ bool geometry(uint64_t xi, uint64_t yi, uint64_t xj, 
   const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
   const bool same = sidi == sidj;
   const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
-  const bool ok = valid && !((same && dr == 0) || dq <= 0) && !((same && dq > max_dist_y) || dq > max_dist_x) &&
-                  !(same && dd > bw) && !(n_segs > 1 && same && dr > max_dist_y);  // is_cdna = 0
+  // bitwise predicates and selects throughout: per-lane branches would cost exec-mask regions
+  const bool ok = valid & !((same & (dr == 0)) | (dq <= 0)) & !((same & (dq > max_dist_y)) | (dq > max_dist_x)) &
+                  !(same & (dd > bw)) & !((n_segs > 1) & same & (dr > max_dist_y));  // is_cdna = 0
   const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
   const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
   const int c_lin = (int)((double)dd * .01 * avg_qspan);
-  int32_t s0 = min_d > q_span ? q_span : min_d;
-  int gap_cost;
-  if (!same) {
-    s0 += dr == 0 ? 1 : 0;
-    gap_cost = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
-  } else {
-    gap_cost = c_lin + (log_dd >> 1);
-  }
+  const int32_t s0 = min_d > q_span ? q_span : min_d;
+  // different sequences: +1 on dr == 0 and gap min(c_lin, log_dd) unless dr == 0; same: c_lin + log_dd/2
+  const int32_t gap_diff = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
+  const int32_t gap_same = c_lin + (log_dd >> 1);
+  const int32_t bonus = (!same & (dr == 0)) ? 1 : 0;
   // (int)((double)gap_cost * gap_scale + .499) with gap_scale == 1.0f (host_kernel.cpp:36) is
   // gap_cost itself for 0 <= gap_cost < 2^31
-  sg = s0 - gap_cost;
+  sg = s0 + bonus - (same ? gap_same : gap_diff);
   return ok;
 }
 
+constexpr int32_t kNoCand = INT_MIN;  // sg of a filtered candidate (producer -> consumer)
+
 // One 64-candidate step in visiting order (lane l = j = jtop - l): running max_f, n_skip, the
-// break and the targets/stamps. Updates M, J, N; returns the break lane (64 = none).
-__device__ __forceinline__ int resolve_step(int32_t sc, bool ok, bool valid, int32_t pj, int64_t j, int64_t jtop,
-                                            int64_t st, uint32_t stamp, int lane, int32_t *__restrict__ target,
-                                            int64_t i, uint32_t *S, int32_t &M, int64_t &J, int32_t &N,
-                                            unsigned long long &vis) {
-  // "targets[j] == i": stamps from visited j' > j with parents[j'] == j
-  if (ok && pj >= st) S[pj & (kRing - 1)] = stamp;
-  const bool tgt = valid && S[j & (kRing - 1)] == stamp;
-  const int32_t mx = scan_max(ok ? sc : INT_MIN);  // inclusive max scan
+// break and the targets/stamps. sc is INT_MIN on filtered lanes (ok false). Updates M, J, N;
+// returns whether the step broke. Indices are int32 (calls hold < 2^30 anchors, checked at batch
+// creation) so uniform compares stay on the SALU, and the step has no exec-mask branch: lanes with
+// nothing to mark stamp a private dummy word S[kRing + lane], and the targets store is a buffer
+// store whose disabled lanes carry an out-of-range offset.
+__device__ __forceinline__ bool resolve_step(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, uint32_t stamp,
+                                             int lane, int32_t neg_lane, __amdgpu_buffer_rsrc_t trs, int32_t i,
+                                             uint32_t *S, int32_t &M, int32_t &J, int32_t &N, uint32_t &vis) {
+  // "targets[j] == i": stamps from visited j' > j with parents[j'] == j. A stamp can only match a
+  // lane whose j >= st (|pj - j| < kRing, so equal ring slots mean pj == j), so no validity test
+  S[(ok & (pj >= st)) ? (pj & (kRing - 1)) : kRing + lane] = stamp;
+  const bool tgt = S[(jtop - lane) & (kRing - 1)] == stamp;
+  const int32_t mx = scan_max(sc);  // inclusive max scan
   const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
-  const bool upd = ok && sc > before;
+  const bool upd = sc > before;  // false on filtered lanes: before >= M >= 0 > INT_MIN
+  const bool plus = ok & !upd & tgt;
+  const uint64_t um_all = __builtin_amdgcn_ballot_w64(upd), pm = __builtin_amdgcn_ballot_w64(plus);
   // n_skip after lane l as a reflected walk: steps +1 (target, no update), -1 floored at 0 (update),
-  // so n_l = max(N + D_l, D_l - min_{k<=l} D_k) with D_l the inclusive step sum -- D from two
-  // ballots and mbcnt, the running minimum from one DPP scan
-  const bool plus = ok && !upd && tgt;
-  const uint64_t pm = __ballot(plus), um_all = __ballot(upd);
-  const int32_t D = incl_count(pm, lane) - incl_count(um_all, lane);
+  // so n_l = max(N + D_l, D_l - min_{k<=l} D_k) with D_l the inclusive step sum. Exclusive part:
+  // mbcnt(pm) - mbcnt(um) = mbcnt(pm) + mbcnt(~um) - lane, one mbcnt chain
+  const uint64_t num = ~um_all;
+  const int32_t d_ex = (int32_t)__builtin_amdgcn_mbcnt_hi(
+      (uint32_t)(num >> 32),
+      __builtin_amdgcn_mbcnt_lo((uint32_t)num, __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)pm, (uint32_t)neg_lane))));
+  const int32_t D = d_ex + (plus ? 1 : (upd ? -1 : 0));
   const int32_t n_after = max(N + D, D - scan_min(D));
-  const bool brk = plus && n_after > kMaxSkip;
-  const uint64_t bm = __ballot(brk);
-  const int bl = bm ? __builtin_ctzll(bm) : 64;
-  const int64_t nvalid = min((int64_t)64, jtop - st + 1);
-  vis += (bl < 64) ? (unsigned long long)(bl + 1) : (unsigned long long)nvalid;
-  const uint64_t low = bl >= 64 ? ~0ull : ((1ull << bl) - 1);
-  const uint64_t um = um_all & low;
-  if (um) {
-    const int lu = 63 - __builtin_clzll(um);
-    J = jtop - lu;
-    M = __builtin_amdgcn_readlane(mx, lu);
-  }
-  if (ok && lane < bl && pj >= 0) target[pj] = (int32_t)i;
+  const uint64_t bm = __builtin_amdgcn_ballot_w64(plus & (n_after > kMaxSkip));
+  const uint64_t below = (bm - 1) & ~bm;  // lanes before the break (all lanes when none)
+  const int32_t nvalid = min(64, jtop - st + 1);
+  vis += bm ? (uint32_t)__builtin_ctzll(bm) + 1 : (uint32_t)nvalid;
+  const uint64_t um = um_all & below;
+  const int lu = 63 - __builtin_clzll(um | 1);  // last improving lane before the break (when um != 0)
+  const int32_t m_lu = __builtin_amdgcn_readlane(mx, lu);
+  J = um ? jtop - lu : J;
+  M = um ? m_lu : M;
+  const bool wt = ok & (bool)((below >> lane) & 1) & (pj >= 0);
+  __builtin_amdgcn_raw_buffer_store_b32(i, trs, wt ? (uint32_t)pj * 4u : 0xFFFFFFFFu, 0, 0);
   N = __builtin_amdgcn_readlane(n_after, 63);
-  return bl;
+  return bm != 0;
 }
 
 // Producer -> consumer hand-off, one slot per anchor i: the geometry of its first 64 candidates.
+// seq = i + 1 is written last and read first, so a slot whose seq matches is complete.
 constexpr int kSlots = 16;
 struct Slot {
-  int32_t sg[64];
-  uint64_t okmask;
-  int64_t st;
-  uint64_t xi, yi;
+  int32_t sg[64];  // kNoCand for filtered candidates
+  int32_t seq, st, q_span, pad;
 };
+
+// LDS counters are read by every lane; the count is uniform, so take it into an SGPR
+__device__ __forceinline__ int32_t lds_count(int *p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
 
 // Two waves per call. The anchors' pair geometry (filters, gap costs; no scores involved) runs ahead
 // in the producer wave and is handed over through an LDS ring; the consumer wave keeps only the
 // score-dependent sequential part (max_f / n_skip scans, break, targets, outputs), so the critical
-// path of a long call is roughly halved. Hand-off words are LDS counters polled with s_sleep.
+// path of a long call is roughly halved. The consumer reads slot i+1 during step i and validates it
+// by its seq word at step i+1; the producer polls the consumer's `consumed` count with s_sleep.
+// PROF adds phase clocks (GB_CHAIN_PROF=1): head, steps, tail, nsteps, slot misses, miss ticks.
+template <bool PROF>
 __global__ __launch_bounds__(128) void chain_kernel(Args A) {
-  __shared__ uint32_t S[kRing];
+  __shared__ uint32_t S[kRing + 64];
   __shared__ Slot ring[kSlots];
-  __shared__ int produced, consumed;
+  __shared__ int consumed;
   const int c = A.order[blockIdx.x];
   const int lane = threadIdx.x & 63;
-  const bool producer = threadIdx.x >= 64;
+  const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;  // wave-uniform role
   const int64_t o = A.offsets[c];
-  const int64_t n = A.offsets[c + 1] - o;
+  const int32_t n = __builtin_amdgcn_readfirstlane((int32_t)(A.offsets[c + 1] - o));
   const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
   const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
   const double avg_qspan = (double)A.avg_qspan[c];
@@ -208,36 +222,36 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   const const_u64 *XC = (const const_u64 *)X, *YC = (const const_u64 *)Y;
   int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
 
-  for (int k = threadIdx.x; k < kRing; k += 128) S[k] = 0;
-  for (int64_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
-  if (threadIdx.x == 0) produced = consumed = 0;
+  for (int k = threadIdx.x; k < kRing + 64; k += 128) S[k] = 0;
+  for (int32_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
+  if (threadIdx.x < kSlots) ring[threadIdx.x].seq = 0;
+  if (threadIdx.x == 0) consumed = 0;
   __builtin_amdgcn_s_waitcnt(0);  // zeroing stores complete before any later targets store
   __syncthreads();
 
   if (producer) {
     // ---------------- producer: geometry of anchor i against i-1-lane --------------------------
     uint64_t wx = 0, wy = 0;  // lane l: anchor i-1-l
-    int64_t st = 0;
-    for (int64_t i = 0; i < n; i++) {
+    int32_t st = 0;
+    for (int32_t iv = 0; iv < n; iv++) {
+      // opaque to loop strength reduction, which otherwise derives i from the per-lane i-1-lane
+      // (a VGPR induction variable) and turns every uniform load below into a vector load
+      const int32_t i = __builtin_amdgcn_readfirstlane(iv);
       const uint64_t xi = XC[i], yi = YC[i];
       while (st < i && xi > XC[st] + (uint64_t)(int64_t)max_dist_x) ++st;
       if (i - st > kMaxIter) st = i - kMaxIter;
       int32_t sg;
       const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
-      const uint64_t okm = __ballot(ok);
       // wait for a free slot
-      while (i - (int64_t)__hip_atomic_load(&consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= kSlots)
-        __builtin_amdgcn_s_sleep(1);
+      while (i - lds_count(&consumed) >= kSlots) __builtin_amdgcn_s_sleep(1);
       Slot &sl = ring[i & (kSlots - 1)];
-      sl.sg[lane] = sg;
+      sl.sg[lane] = ok ? sg : kNoCand;
       if (lane == 0) {
-        sl.okmask = okm;
         sl.st = st;
-        sl.xi = xi;
-        sl.yi = yi;
+        sl.q_span = (int32_t)(yi >> 32 & 0xff);
       }
-      __builtin_amdgcn_s_waitcnt(0);  // slot contents land before the count that publishes them
-      if (lane == 0) __hip_atomic_store(&produced, (int)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // slot contents land before the seq that publishes them
+      if (lane == 0) __hip_atomic_store(&sl.seq, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       wx = dpp_shr_u64(wx, xi);
       wy = dpp_shr_u64(wy, yi);
     }
@@ -245,99 +259,120 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   }
 
   // ---------------- consumer ---------------------------------------------------------------------
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(target, (short)0, n * 4, 0x00020000);
+  const int32_t neg_lane = -lane;
   int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l
   unsigned long long vis = 0;
-  unsigned long long c_head = 0, c_step = 0, c_tail = 0, n_step = 0, t_0 = 0, t_1 = 0;
-  const bool prof = A.prof != nullptr;
-  for (int64_t i = 0; i < n; i++) {
-    if (prof) t_0 = __builtin_amdgcn_s_memtime();
-    if ((i & 63) == 0 && i > 0) {  // flush the window: anchors i-64 .. i-1 (lane l: i-1-l)
-      score[i - 1 - lane] = ws;
-      parent[i - 1 - lane] = wpar;
-      peak[i - 1 - lane] = wpk;
-      __builtin_amdgcn_s_waitcnt(0);  // flushed anchors are in L2 before any older-candidate read
-    }
-    while ((int64_t)__hip_atomic_load(&produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= i)
-      __builtin_amdgcn_s_sleep(1);
-    const Slot &sl = ring[i & (kSlots - 1)];
-    const int32_t sg = sl.sg[lane];
-    const bool ok = (sl.okmask >> lane) & 1;
-    const int64_t st = sl.st;
-    const uint64_t xi = sl.xi, yi = sl.yi;
-    __builtin_amdgcn_s_waitcnt(0);
-    if (lane == 0) __hip_atomic_store(&consumed, (int)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const int32_t q_span = (int32_t)(yi >> 32 & 0xff);
-    int32_t M = q_span, N = 0;
-    int64_t J = -1;
-    const uint32_t stamp = (uint32_t)(i + 1);
-    if (prof) {
-      t_1 = __builtin_amdgcn_s_memtime();
-      c_head += t_1 - t_0;
-      t_0 = t_1;
-    }
-    const int64_t jtop = i - 1;
-    int bl = 64;
-    if (jtop >= st) {
-      if (prof) ++n_step;
-      const int64_t j = jtop - lane;
-      bl = resolve_step(ok ? sg + ws : INT_MIN, ok, j >= st, wpar, j, jtop, st, stamp, lane, target, i, S, M, J, N, vis);
-    }
-    if (bl == 64 && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
-      for (int64_t jt = jtop - 64; jt >= st; jt -= 64) {
-        if (prof) ++n_step;
-        const int64_t jj = jt - lane;
-        const bool v = jj >= st;
-        uint64_t xj = 0, yj = 0;
-        int32_t scj = 0, pj = -1;
-        if (v) {
-          xj = X[jj];
-          yj = Y[jj];
-          scj = load_l2(score + jj);
-          pj = load_l2(parent + jj);
+  unsigned long long c_head = 0, c_step = 0, c_tail = 0, n_step = 0, n_miss = 0, c_miss = 0, t_0 = 0, t_1 = 0;
+  // slot i is read during step i-1 (header first: LDS executes a wave's reads in order, so a
+  // matching seq means the sg read after it saw the complete slot)
+  // volatile LDS (address space 3) reads: kept in program order (seq before sg) and still ds_read
+  typedef int32_t v4i __attribute__((ext_vector_type(4)));
+  typedef volatile __attribute__((address_space(3))) v4i lds_v4i;
+  typedef volatile __attribute__((address_space(3))) int32_t lds_i32;
+  v4i hdr = *(lds_v4i *)&ring[0].seq;
+  int32_t psg = *(lds_i32 *)&ring[0].sg[lane];
+  for (int32_t base = 0; base < n; base += 64) {
+    const int32_t cnt = min(64, n - base);
+    for (int32_t k = 0; k < cnt; k++) {
+      const int32_t i = __builtin_amdgcn_readfirstlane(base + k);
+      if (PROF) t_0 = __builtin_amdgcn_s_memtime();
+      int32_t st, q_span, sg;
+      if (__builtin_amdgcn_readfirstlane(hdr.x) == i + 1) {
+        st = __builtin_amdgcn_readfirstlane(hdr.y);
+        q_span = __builtin_amdgcn_readfirstlane(hdr.z);
+        sg = psg;
+      } else {  // the producer was behind when the slot was read ahead: wait for it, read again
+        if (PROF) {
+          ++n_miss;
+          t_1 = __builtin_amdgcn_s_memtime();
         }
-        int32_t sgo;
-        const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
-        if (resolve_step(oko ? sgo + scj : INT_MIN, oko, v, pj, jj, jt, st, stamp, lane, target, i, S, M, J, N,
-                         vis) < 64)
-          break;
+        Slot &sl = ring[i & (kSlots - 1)];
+        while (lds_count(&sl.seq) != i + 1) __builtin_amdgcn_s_sleep(1);
+        if (PROF) c_miss += __builtin_amdgcn_s_memtime() - t_1;
+        st = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.st);
+        q_span = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.q_span);
+        sg = *(lds_i32 *)&sl.sg[lane];
       }
+      // free slot i (its reads were issued before this write, and LDS runs them in order), then
+      // read slot i+1 ahead; its latency overlaps this step
+      if (lane == 0) __hip_atomic_store(&consumed, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      {
+        Slot &nl = ring[(i + 1) & (kSlots - 1)];
+        hdr = *(lds_v4i *)&nl.seq;
+        psg = *(lds_i32 *)&nl.sg[lane];
+      }
+      const bool ok = sg != kNoCand;
+      int32_t M = q_span, N = 0, J = -1;
+      const uint32_t stamp = (uint32_t)(i + 1);
+      uint32_t vis_i = 0;
+      if (PROF) {
+        t_1 = __builtin_amdgcn_s_memtime();
+        c_head += t_1 - t_0;
+        t_0 = t_1;
+      }
+      const int32_t jtop = i - 1;
+      bool brk = false;
+      if (jtop >= st) {
+        if (PROF) ++n_step;
+        const int32_t sc = ok ? (int32_t)((uint32_t)sg + (uint32_t)ws) : INT_MIN;
+        brk = resolve_step(sc, ok, wpar, jtop, st, stamp, lane, neg_lane, trs, i, S, M, J, N, vis_i);
+      }
+      if (!brk && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
+        const uint64_t xi = X[i], yi = Y[i];
+        for (int32_t jt = jtop - 64; jt >= st; jt -= 64) {
+          if (PROF) ++n_step;
+          const int32_t jj = jt - lane;
+          const bool v = jj >= st;
+          uint64_t xj = 0, yj = 0;
+          int32_t scj = 0, pj = -1;
+          if (v) {
+            xj = X[jj];
+            yj = Y[jj];
+            scj = load_l2(score + jj);
+            pj = load_l2(parent + jj);
+          }
+          int32_t sgo;
+          const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
+          if (resolve_step(oko ? sgo + scj : INT_MIN, oko, pj, jt, st, stamp, lane, neg_lane, trs, i, S, M, J, N,
+                           vis_i))
+            break;
+        }
+      }
+      vis += vis_i;
+      if (PROF) {
+        t_1 = __builtin_amdgcn_s_memtime();
+        c_step += t_1 - t_0;
+        t_0 = t_1;
+      }
+      // peak of the parent: from the register window when J >= i-64, else (rare) from memory
+      const int32_t dJ = i - 1 - J;
+      int32_t pkJ = __builtin_amdgcn_readlane(wpk, dJ & 63);
+      if (J >= 0 && dJ > 63) pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
+      const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
+      ws = dpp_shr_i32(ws, M);
+      wpar = dpp_shr_i32(wpar, J);
+      wpk = dpp_shr_i32(wpk, pki);
+      if (PROF) c_tail += __builtin_amdgcn_s_memtime() - t_0;
     }
-    if (prof) {
-      t_1 = __builtin_amdgcn_s_memtime();
-      c_step += t_1 - t_0;
-      t_0 = t_1;
+    // flush the window: anchors base .. base+cnt-1 (lane l: base+cnt-1-l)
+    if (lane < cnt) {
+      score[base + cnt - 1 - lane] = ws;
+      parent[base + cnt - 1 - lane] = wpar;
+      peak[base + cnt - 1 - lane] = wpk;
     }
-    int32_t pkJ = 0;
-    if (J >= 0) {
-      if (J >= i - 64)
-        pkJ = __builtin_amdgcn_readlane(wpk, (int)(i - 1 - J));
-      else  // rare: consume the load inside the branch so the common path carries no vmcnt wait
-        pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
-    }
-    const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
-    ws = dpp_shr_i32(ws, M);
-    wpar = dpp_shr_i32(wpar, (int32_t)J);
-    wpk = dpp_shr_i32(wpk, pki);
-    if (prof) c_tail += __builtin_amdgcn_s_memtime() - t_0;
+    __builtin_amdgcn_s_waitcnt(0);  // flushed anchors are in L2 before any older-candidate read
   }
-  // final flush: anchors max(0, n - r) .. n-1 with r = n mod 64 (or 64)
-  {
-    const int64_t r = ((n - 1) & 63) + 1;
-    if (lane < r) {
-      score[n - 1 - lane] = ws;
-      parent[n - 1 - lane] = wpar;
-      peak[n - 1 - lane] = wpk;
-    }
-  }
-  // wave-reduce the visited count
-  if (prof && lane == 0) {
+  if (PROF && lane == 0) {
     atomicAdd(A.prof + 0, c_head);
     atomicAdd(A.prof + 1, c_step);
     atomicAdd(A.prof + 2, c_tail);
     atomicAdd(A.prof + 3, n_step);
+    atomicAdd(A.prof + 4, n_miss);
+    atomicAdd(A.prof + 5, c_miss);
   }
-  for (int d = 32; d >= 1; d >>= 1) vis += __shfl_xor(vis, d);
-  if (lane == 0) atomicAdd(A.visited, vis / 64);
+  // every lane accumulated the same (uniform) count
+  if (lane == 0) atomicAdd(A.visited, vis);
 }
 
 }  // namespace gbchain
@@ -353,7 +388,7 @@ int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *a
   const int64_t na = offsets[ncalls];
   GB_ARG(offsets[0] == 0 && na >= 0 && (na == 0 || (x && y)), "gb_chain_batch_create: bad offsets");
   for (int64_t c = 0; c < ncalls; c++)
-    GB_ARG(offsets[c + 1] >= offsets[c] && offsets[c + 1] - offsets[c] < (1ll << 31),
+    GB_ARG(offsets[c + 1] >= offsets[c] && offsets[c + 1] - offsets[c] < (1ll << 30),
            "gb_chain_batch_create: call %lld has a bad anchor range", (long long)c);
   GB_ARG(ncalls == 0 || (avg_qspan && params4), "gb_chain_batch_create: null parameters");
   // longest calls first: the grid is dispatched in order, so the critical path starts first
@@ -415,20 +450,23 @@ int gb_chain_batch_run(gb_chain_batch *B) {
     A.prof = nullptr;
     const char *pe = getenv("GB_CHAIN_PROF");
     if (pe && *pe == '1') {
-      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 4 * sizeof(unsigned long long)));
-      GB_HIP(hipMemsetAsync(B->d_prof, 0, 4 * sizeof(unsigned long long), B->stream));
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 6 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 6 * sizeof(unsigned long long), B->stream));
       A.prof = B->d_prof;
     }
-    hipLaunchKernelGGL(gbchain::chain_kernel, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
+    if (A.prof)
+      hipLaunchKernelGGL(gbchain::chain_kernel<true>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
+    else
+      hipLaunchKernelGGL(gbchain::chain_kernel<false>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   if (B->d_prof && getenv("GB_CHAIN_PROF")) {
-    unsigned long long h[4];
+    unsigned long long h[6];
     GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
-    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu\n", h[0], h[1],
-            h[2], h[3]);
+    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu; slot misses %llu (%llu ticks)\n",
+            h[0], h[1], h[2], h[3], h[4], h[5]);
   }
   B->ran = true;
   return GB_OK;

@@ -3,12 +3,23 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_chain_bt.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/chain_bt_test.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/chain_bt_test.log; exit 1; }
-tail -1 gpurun_out/chain_bt_test.log
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bt -o run -- python3 bench.py --only chain --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bt.json 2> gpurun_out/prof_bt.err || { echo "failed"; tail gpurun_out/prof_bt.err; exit 1; }
-python -c "
-import csv,json
-for r in csv.DictReader(open('gpurun_out/prof_bt/run_kernel_stats.csv')):
-    n=r['Name'].split('(')[0][-40:]
-    if float(r['AverageNs'])>50000: print(f\"{n:42s} {float(r['AverageNs'])/1e6:8.3f} ms\")
-d=json.loads(open('gpurun_out/prof_bt.json').read().strip().splitlines()[-1]); print('bt', d['chain']['backtrack']['value'], d['chain']['backtrack']['kernels_ms'])"
+timeout -k 10 400 python -u -m pytest tests/test_chain.py tests/test_chain_bt.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/chain_test.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/chain_test.log; exit 1; }
+tail -1 gpurun_out/chain_test.log
+timeout -k 10 300 python tools/chain_probe.py > gpurun_out/chain_probe.log 2>&1 || { tail gpurun_out/chain_probe.log; exit 1; }
+cat gpurun_out/chain_probe.log
+GB_CHAIN_PROF=1 timeout -k 10 300 python - > gpurun_out/chain_prof.log 2>&1 <<'PY' || { tail gpurun_out/chain_prof.log; exit 1; }
+import sys; sys.path.insert(0, '.'); sys.path.insert(0, 'tools')
+import numpy as np
+from genomicsbench_palisade_amd import chain, gen, set_device
+set_device(0)
+calls = gen.chain_dataset("large", seed=5)
+lens = calls.offsets[1:] - calls.offsets[:-1]
+c = int(np.argmax(lens))
+o0, o1 = calls.offsets[c], calls.offsets[c + 1]
+sub = gen.ChainCalls(np.array([0, o1 - o0]), calls.x[o0:o1], calls.y[o0:o1], calls.avg_qspan[c:c+1], calls.params4[c:c+1])
+b = chain.ChainBatch(sub)
+for _ in range(2):
+    b.run(); b.sync()
+print("longest call", o1 - o0, "anchors", b.timing(), "ms")
+PY
+cat gpurun_out/chain_prof.log
