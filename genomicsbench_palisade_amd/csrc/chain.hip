@@ -45,7 +45,8 @@ struct Args {
   const int32_t *order;  // calls, longest first
   int32_t *score, *parent, *target, *peak;
   unsigned long long *visited;
-  unsigned long long *prof;  // optional phase clocks (GB_CHAIN_PROF=1): head, steps, tail, nsteps
+  unsigned long long *prof;  // optional phase clocks (GB_CHAIN_PROF=1), see chain_kernel
+  int32_t prof_call;         // the call whose consumer also records shader-clock and 100 MHz ticks
 };
 
 __device__ __forceinline__ int ilog2_32(uint32_t v) { return 31 - __clz((int)v); }  // v > 0 (LogTable256)
@@ -194,6 +195,11 @@ struct Slot {
   int32_t seq, st, q_span, pad;
 };
 
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32;
+}
+
 // LDS counters are read by every lane; the count is uniform, so take it into an SGPR
 __device__ __forceinline__ int32_t lds_count(int *p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -204,11 +210,13 @@ __device__ __forceinline__ int32_t lds_count(int *p) {
 // score-dependent sequential part (max_f / n_skip scans, break, targets, outputs), so the critical
 // path of a long call is roughly halved. The consumer reads slot i+1 during step i and validates it
 // by its seq word at step i+1; the producer polls the consumer's `consumed` count with s_sleep.
-// PROF adds phase clocks (GB_CHAIN_PROF=1): head, steps, tail, nsteps, slot misses, miss ticks.
-template <bool PROF>
+// PROF (GB_CHAIN_PROF): 1 = start/end stamps (100 MHz) of the first/longest call and of the
+// whole grid; 2 = also phase clocks: head, steps, tail, nsteps, slot misses, miss ticks.
+template <int PROF>
 __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   __shared__ uint32_t S[kRing + 64];
   __shared__ Slot ring[kSlots];
+  __shared__ uint64_t xyblk[2][2][64];  // producer's staged anchor blocks: [b & 1][x | y][k]
   __shared__ int consumed;
   const int c = A.order[blockIdx.x];
   const int lane = threadIdx.x & 63;
@@ -233,17 +241,43 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     // ---------------- producer: geometry of anchor i against i-1-lane --------------------------
     uint64_t wx = 0, wy = 0;  // lane l: anchor i-1-l
     int32_t st = 0;
+    const bool pc = PROF == 2 && c == A.prof_call;
+    unsigned long long p_load = 0, p_wait = 0, t0 = 0;
+    // Anchors x/y reach the producer through LDS, a 64-anchor block ahead: at the start of block
+    // b the block loaded at the start of b-1 (one coalesced load per array; its only wait is here)
+    // goes into xy[b & 1], and block b+1 is requested. No load sits on the per-anchor path, which
+    // keeps the producer ahead when L2/HBM are busy with other calls. The window start's x is kept
+    // in SGPRs and refreshed by a scalar load only when st advances.
+    uint64_t nx = X[min(lane, n - 1)], ny = Y[min(lane, n - 1)];
+    uint64_t xst = n > 0 ? XC[0] : 0;
     for (int32_t iv = 0; iv < n; iv++) {
       // opaque to loop strength reduction, which otherwise derives i from the per-lane i-1-lane
-      // (a VGPR induction variable) and turns every uniform load below into a vector load
+      // (a VGPR induction variable) and turns every uniform value below into a vector one
       const int32_t i = __builtin_amdgcn_readfirstlane(iv);
-      const uint64_t xi = XC[i], yi = YC[i];
-      while (st < i && xi > XC[st] + (uint64_t)(int64_t)max_dist_x) ++st;
-      if (i - st > kMaxIter) st = i - kMaxIter;
+      if (pc) t0 = __builtin_amdgcn_s_memtime();
+      if ((i & 63) == 0) {
+        xyblk[(i >> 6) & 1][0][lane] = nx;
+        xyblk[(i >> 6) & 1][1][lane] = ny;
+        nx = X[min(i + 64 + lane, n - 1)];
+        ny = Y[min(i + 64 + lane, n - 1)];
+      }
+      const uint64_t xi = rfl64(xyblk[(i >> 6) & 1][0][i & 63]), yi = rfl64(xyblk[(i >> 6) & 1][1][i & 63]);
+      while (st < i && xi > xst + (uint64_t)(int64_t)max_dist_x) xst = XC[++st];
+      if (i - st > kMaxIter) {  // rare: > max_iter candidates in range
+        st = i - kMaxIter;
+        xst = XC[st];
+      }
+      if (pc) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        p_load += t1 - t0;
+      }
       int32_t sg;
       const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
       // wait for a free slot
+      if (pc) t0 = __builtin_amdgcn_s_memtime();
       while (i - lds_count(&consumed) >= kSlots) __builtin_amdgcn_s_sleep(1);
+      if (pc) p_wait += __builtin_amdgcn_s_memtime() - t0;
       Slot &sl = ring[i & (kSlots - 1)];
       sl.sg[lane] = ok ? sg : kNoCand;
       if (lane == 0) {
@@ -255,10 +289,15 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       wx = dpp_shr_u64(wx, xi);
       wy = dpp_shr_u64(wy, yi);
     }
+    if (pc && lane == 0) {
+      atomicAdd(A.prof + 12, p_load);
+      atomicAdd(A.prof + 13, p_wait);
+    }
     return;
   }
 
   // ---------------- consumer ---------------------------------------------------------------------
+  const bool pc = PROF == 2 && c == A.prof_call;  // phase clocks for the profiled call only
   const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(target, (short)0, n * 4, 0x00020000);
   const int32_t neg_lane = -lane;
   int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l
@@ -272,24 +311,29 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   typedef volatile __attribute__((address_space(3))) int32_t lds_i32;
   v4i hdr = *(lds_v4i *)&ring[0].seq;
   int32_t psg = *(lds_i32 *)&ring[0].sg[lane];
+  unsigned long long clk0 = 0, rt0 = 0;
+  if (PROF) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   for (int32_t base = 0; base < n; base += 64) {
     const int32_t cnt = min(64, n - base);
     for (int32_t k = 0; k < cnt; k++) {
       const int32_t i = __builtin_amdgcn_readfirstlane(base + k);
-      if (PROF) t_0 = __builtin_amdgcn_s_memtime();
+      if (pc) t_0 = __builtin_amdgcn_s_memtime();
       int32_t st, q_span, sg;
       if (__builtin_amdgcn_readfirstlane(hdr.x) == i + 1) {
         st = __builtin_amdgcn_readfirstlane(hdr.y);
         q_span = __builtin_amdgcn_readfirstlane(hdr.z);
         sg = psg;
       } else {  // the producer was behind when the slot was read ahead: wait for it, read again
-        if (PROF) {
+        if (pc) {
           ++n_miss;
           t_1 = __builtin_amdgcn_s_memtime();
         }
         Slot &sl = ring[i & (kSlots - 1)];
         while (lds_count(&sl.seq) != i + 1) __builtin_amdgcn_s_sleep(1);
-        if (PROF) c_miss += __builtin_amdgcn_s_memtime() - t_1;
+        if (pc) c_miss += __builtin_amdgcn_s_memtime() - t_1;
         st = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.st);
         q_span = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.q_span);
         sg = *(lds_i32 *)&sl.sg[lane];
@@ -306,7 +350,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       int32_t M = q_span, N = 0, J = -1;
       const uint32_t stamp = (uint32_t)(i + 1);
       uint32_t vis_i = 0;
-      if (PROF) {
+      if (pc) {
         t_1 = __builtin_amdgcn_s_memtime();
         c_head += t_1 - t_0;
         t_0 = t_1;
@@ -314,14 +358,17 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       const int32_t jtop = i - 1;
       bool brk = false;
       if (jtop >= st) {
-        if (PROF) ++n_step;
+        if (pc) ++n_step;
         const int32_t sc = ok ? (int32_t)((uint32_t)sg + (uint32_t)ws) : INT_MIN;
         brk = resolve_step(sc, ok, wpar, jtop, st, stamp, lane, neg_lane, trs, i, S, M, J, N, vis_i);
       }
       if (!brk && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
+        // the wave's flushed score/parent stores reach L2 before these sc1 reads of them (the
+        // drain sits here, not at every flush, so the common path never waits on a store)
+        __builtin_amdgcn_s_waitcnt(0);
         const uint64_t xi = X[i], yi = Y[i];
         for (int32_t jt = jtop - 64; jt >= st; jt -= 64) {
-          if (PROF) ++n_step;
+          if (pc) ++n_step;
           const int32_t jj = jt - lane;
           const bool v = jj >= st;
           uint64_t xj = 0, yj = 0;
@@ -340,7 +387,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
         }
       }
       vis += vis_i;
-      if (PROF) {
+      if (pc) {
         t_1 = __builtin_amdgcn_s_memtime();
         c_step += t_1 - t_0;
         t_0 = t_1;
@@ -353,7 +400,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       ws = dpp_shr_i32(ws, M);
       wpar = dpp_shr_i32(wpar, J);
       wpk = dpp_shr_i32(wpk, pki);
-      if (PROF) c_tail += __builtin_amdgcn_s_memtime() - t_0;
+      if (pc) c_tail += __builtin_amdgcn_s_memtime() - t_0;
     }
     // flush the window: anchors base .. base+cnt-1 (lane l: base+cnt-1-l)
     if (lane < cnt) {
@@ -361,15 +408,27 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       parent[base + cnt - 1 - lane] = wpar;
       peak[base + cnt - 1 - lane] = wpk;
     }
-    __builtin_amdgcn_s_waitcnt(0);  // flushed anchors are in L2 before any older-candidate read
   }
   if (PROF && lane == 0) {
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+    atomicMin(A.prof + 8, rt0);
+    atomicMax(A.prof + 11, rt1);
+    if (c == A.prof_call) {
+      atomicAdd(A.prof + 9, rt0);
+      atomicAdd(A.prof + 10, rt1);
+    }
+  }
+  if (pc && lane == 0) {
     atomicAdd(A.prof + 0, c_head);
     atomicAdd(A.prof + 1, c_step);
     atomicAdd(A.prof + 2, c_tail);
     atomicAdd(A.prof + 3, n_step);
     atomicAdd(A.prof + 4, n_miss);
     atomicAdd(A.prof + 5, c_miss);
+    if (c == A.prof_call) {
+      atomicAdd(A.prof + 6, __builtin_amdgcn_s_memtime() - clk0);
+      atomicAdd(A.prof + 7, __builtin_amdgcn_s_memrealtime() - rt0);
+    }
   }
   // every lane accumulated the same (uniform) count
   if (lane == 0) atomicAdd(A.visited, vis);
@@ -448,25 +507,36 @@ int gb_chain_batch_run(gb_chain_batch *B) {
     A.peak = B->d_out + 3 * nn;
     A.visited = B->d_vis;
     A.prof = nullptr;
+    A.prof_call = -1;
     const char *pe = getenv("GB_CHAIN_PROF");
-    if (pe && *pe == '1') {
-      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 6 * sizeof(unsigned long long)));
-      GB_HIP(hipMemsetAsync(B->d_prof, 0, 6 * sizeof(unsigned long long), B->stream));
+    const int prof = (pe && (*pe == '1' || *pe == '2')) ? *pe - '0' : 0;
+    if (prof) {
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 14 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 14 * sizeof(unsigned long long), B->stream));
+      GB_HIP(hipMemsetAsync(B->d_prof + 8, 0xff, sizeof(unsigned long long), B->stream));
       A.prof = B->d_prof;
+      int32_t c0 = 0;
+      GB_HIP(hipMemcpy(&c0, B->d_order, sizeof(c0), hipMemcpyDeviceToHost));
+      A.prof_call = c0;
     }
-    if (A.prof)
-      hipLaunchKernelGGL(gbchain::chain_kernel<true>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
+    if (prof == 2)
+      hipLaunchKernelGGL(gbchain::chain_kernel<2>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
+    else if (prof == 1)
+      hipLaunchKernelGGL(gbchain::chain_kernel<1>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
     else
-      hipLaunchKernelGGL(gbchain::chain_kernel<false>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
+      hipLaunchKernelGGL(gbchain::chain_kernel<0>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
     GB_HIP(hipGetLastError());
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   if (B->d_prof && getenv("GB_CHAIN_PROF")) {
-    unsigned long long h[6];
+    unsigned long long h[14];
     GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
-    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu; slot misses %llu (%llu ticks)\n",
-            h[0], h[1], h[2], h[3], h[4], h[5]);
+    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu; slot misses %llu (%llu ticks); "
+            "longest call %llu clk / %llu rt ticks = %.0f MHz\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7],
+            h[7] ? 100.0 * (double)h[6] / (double)h[7] : 0.0);
+    fprintf(stderr, "[chain prof] grid %.3f ms; longest call starts at %.3f ms, ends at %.3f ms; producer load %llu wait %llu\n",
+            (double)(h[11] - h[8]) * 1e-5, (double)(h[9] - h[8]) * 1e-5, (double)(h[10] - h[8]) * 1e-5, h[12], h[13]);
   }
   B->ran = true;
   return GB_OK;
