@@ -227,7 +227,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
   const double avg_qspan = (double)A.avg_qspan[c];
   const uint64_t *X = A.x + o, *Y = A.y + o;
-  const const_u64 *XC = (const const_u64 *)X, *YC = (const const_u64 *)Y;
+  const const_u64 *XC = (const const_u64 *)X;
   int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
 
   for (int k = threadIdx.x; k < kRing + 64; k += 128) S[k] = 0;

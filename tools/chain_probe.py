@@ -2,6 +2,9 @@
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
+import genomicsbench_palisade_amd as gbp
+if os.environ.get("GB_LIBGB"):  # A/B a differently built libgb.so (development aid)
+    gbp.LIBGB = os.path.abspath(os.environ["GB_LIBGB"])
 from genomicsbench_palisade_amd import chain, gen, set_device
 
 set_device(0)
