@@ -45,10 +45,11 @@ BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar in
 PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
-def pmc_traffic(kernel: str):
-    """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE) of `kernel` from the newest committed
-    profiles/*_pmc.json (rocprofv3 PMC passes of this same bench configuration, tools/gpu_prof.sh +
-    tools/pmc_summary.py); None when no profile covers it. PMC cannot run inside the timed process."""
+def pmc_traffic_detail(kernel: str):
+    """Per-launch HBM bytes of `kernel` from the newest committed profiles/*_pmc.json (rocprofv3
+    FETCH_SIZE and WRITE_SIZE passes of this same bench configuration, tools/gpu_prof.sh +
+    tools/pmc_summary.py, fetch corrected by the calibrated factor of the kernel's read class);
+    None when no profile covers it. PMC cannot run inside the timed process."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
     for f in reversed(files):
@@ -56,11 +57,19 @@ def pmc_traffic(kernel: str):
             d = json.load(open(f))
         except Exception:
             continue
-        if kernel in d:
-            return {"bytes": d[kernel]["fetch_bytes"] + d[kernel]["write_bytes"],
-                    "fetch_bytes": d[kernel]["fetch_bytes"], "write_bytes": d[kernel]["write_bytes"],
+        if kernel in d and "fetch_factor" in d[kernel]:
+            k = d[kernel]
+            return {"bytes": k["fetch_bytes"] + k["write_bytes"], "fetch_bytes": k["fetch_bytes"],
+                    "fetch_bytes_raw": k["fetch_bytes_raw"], "fetch_factor": k["fetch_factor"],
+                    "fetch_class": k["fetch_class"], "write_bytes": k["write_bytes"],
                     "source": os.path.relpath(f, ROOT)}
     return None
+
+
+def pmc_traffic(kernel: str):
+    """roofline.traffic: corrected HBM bytes per launch (number), or None."""
+    d = pmc_traffic_detail(kernel)
+    return None if d is None else d["bytes"]
 
 
 def log(msg):
@@ -311,6 +320,7 @@ def bench_chain(args, D, rank, world):
                    "visited_pairs": int(visited), "gpairs_per_s": visited * args.steps * D.world / elapsed / 1e9},
         "roofline": {"bound": "valu", "kernel": "chain_kernel", "achieved": ach / 1e12, "peak": PEAK_CHAIN_OPS / 1e12,
                      "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": pmc_traffic("chain_kernel"),
+                     "traffic_detail": pmc_traffic_detail("chain_kernel"),
                      "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_kernel": ms},
         "cpu_baseline": cpu,
@@ -412,7 +422,8 @@ def bench_bsw(args, D, rank, world):
         "roofline": {"bound": "valu", "kernel": "bsw_lane_kernel<NCH> (+ bsw_extend_kernel for long queries)",
                      "achieved": ach / 1e12,
                      "peak": PEAK_INT_OPS / 1e12, "unit": "T int op/s", "frac": ach / PEAK_INT_OPS,
-                     "traffic": pmc_traffic("bsw_lane_kernel"), "ops_per_cell": BSW_OPS_PER_CELL},
+                     "traffic": pmc_traffic("bsw_lane_kernel"),
+                     "traffic_detail": pmc_traffic_detail("bsw_lane_kernel"), "ops_per_cell": BSW_OPS_PER_CELL},
         "kernels_ms": {"bsw (all launches of a step)": ms},
         "cpu_baseline": cpu,
     }
@@ -465,7 +476,8 @@ def bench_phmm(args, D, rank, world):
     return {
         "value": gcups, "elapsed": elapsed, "ntc": ntc, "cells": cells, "f64_frac": float(used.mean()),
         "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
-                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": pmc_traffic(kern)},
+                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": pmc_traffic(kern),
+                     "traffic_detail": pmc_traffic_detail(kern)},
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
         "cpu_baseline": cpu,
     }
@@ -525,6 +537,7 @@ def bench_fmi(args, D, rank, world):
                    "backwardExt_per_read": calls / len(lens), "index_build_s": round(t_index, 2)},
         "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
                      "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": pmc_traffic("smem_search"),
+                     "traffic_detail": pmc_traffic_detail("smem_search"),
                      "algorithmic_bytes": int(alg_bytes)},
         "kernels_ms": {"smem_search": ms, "smem_search+scan": float(np.mean(kt))},
         "cpu_baseline": cpu,
@@ -574,6 +587,7 @@ def bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens):
                    "coords_per_step": int(ncoords), "lf_steps_per_coord": steps / max(ncoords, 1)},
         "roofline": {"bound": "hbm", "kernel": "sa_walk", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
                      "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": pmc_traffic("sa_walk"),
+                     "traffic_detail": pmc_traffic_detail("sa_walk"),
                      "algorithmic_bytes": int(alg_bytes)},
         "kernels_ms": {"sa_expand+sa_walk": ms},
         "cpu_baseline": cpu,

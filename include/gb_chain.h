@@ -23,7 +23,8 @@ extern "C" {
 
 typedef struct gb_chain_batch gb_chain_batch;
 
-/* Upload a set of calls (anchors sorted by x within each call, as minimap2 produces them). */
+/* Upload a set of calls (anchors sorted by x within each call, as minimap2 produces them; each call
+ * below 2^30 anchors, else GB_ERR_ARG). */
 int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
                           const int32_t *params4, const uint64_t *x, const uint64_t *y,
                           gb_chain_batch **out);

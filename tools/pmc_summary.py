@@ -1,7 +1,13 @@
-"""Summarise rocprofv3 runs of bench.py into profiles/<tag>_pmc.json:
-per hot kernel (fmi pass 1 and pass 2 told apart by grid size) the mean duration, FETCH_SIZE and
-WRITE_SIZE per launch converted from KiB to bytes. No correction factor is applied: the gfx950 x2
-FETCH_SIZE correction of MI355X_MICROARCH.md is calibrated for wide coalesced streaming reads only.
+"""Summarise rocprofv3 runs of bench.py into profiles/<tag>_pmc.json: per hot kernel (fmi pass 1 and
+pass 2 told apart by grid size) the mean duration and the HBM bytes per launch from FETCH_SIZE and
+WRITE_SIZE (separate passes), KiB x 1024.
+
+Correction, as MI355X_MICROARCH.md's HBM section prescribes ("calibrate on a known byte count in
+your own access pattern"), from tools/probes/pmc_calib.hip (profiles/r01g_pmc_calib.txt): WRITE_SIZE
+is exact; FETCH_SIZE counts scattered line-granular reads at their true bytes (random 64-B lines
+1.03, one 8-B word per line 1.00 of the lines, 32-B halves of lines 2.02 = a whole line each) and
+coalesced 16-B/lane streaming reads at 1/2 (the guide's gfx950 case). Each hot kernel's fetch is
+scaled by the factor of its dominant read class (KERNEL_CLASS); the raw counter is kept beside it.
 
     python tools/pmc_summary.py gpurun_out/pmc_fetch_TAG gpurun_out/pmc_write_TAG profiles/TAG_pmc.json
 """
@@ -14,6 +20,19 @@ import sys
 HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
        "smem_search": "smem_search", "chain_kernel": "chain_kernel", "bsw_extend_kernel": "bsw_extend_kernel",
        "bsw_lane_kernel": "bsw_lane_kernel", "sa_walk": "sa_walk"}
+
+FETCH_FACTOR = {"gather": 1.0, "stream": 2.0}
+# dominant read class per kernel: scattered per-lane line requests ("gather") or coalesced
+# per-wave streams ("stream")
+KERNEL_CLASS = {
+    "smem_search": "gather",            # Occ32 blocks at random rows
+    "sa_walk": "gather",                # Occ32 blocks and sampled-SA words at random rows
+    "bsw_lane_kernel": "gather",        # each lane reads its own pair's sequences
+    "bsw_extend_kernel": "stream",      # one pair per wave, lanes over the query
+    "phmm_forward<float>": "stream",    # one testcase per wave, coalesced read/haplotype bytes
+    "phmm_forward<double>": "stream",
+    "chain_kernel": "stream",           # anchors in 64-anchor coalesced blocks
+}
 
 
 def name_of(r):
@@ -52,10 +71,14 @@ def main():
         fb = [v for v, _ in f.get(k, [])]
         wb = [v for v, _ in w.get(k, [])]
         ms = [d for _, d in f.get(k, [])] + [d for _, d in w.get(k, [])]
-        res[k] = {"launches": len(fb), "fetch_bytes": sum(fb) / max(len(fb), 1),
+        raw = sum(fb) / max(len(fb), 1)
+        cls = KERNEL_CLASS.get(k, "gather")
+        res[k] = {"launches": len(fb), "fetch_bytes": raw * FETCH_FACTOR[cls], "fetch_bytes_raw": raw,
+                  "fetch_class": cls, "fetch_factor": FETCH_FACTOR[cls],
                   "write_bytes": sum(wb) / max(len(wb), 1), "mean_ms_under_pmc": sum(ms) / max(len(ms), 1)}
-    res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch, "
-                    "uncorrected (MI355X_MICROARCH.md HBM section)")
+    res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch; fetch "
+                    "scaled by the calibrated factor of the kernel's read class (tools/probes/pmc_calib.hip, "
+                    "profiles/r01g_pmc_calib.txt), write exact")
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
