@@ -4,19 +4,20 @@
 // tools/minimap2-acceleration/kernel/scalar/src/host_kernel.cpp:30-94, with the C integer / double
 // semantics of that source (int64 dr, int32 truncations, (int)(dd * .01 * avg_qspan), no FMA).
 //
-// MI355X design: one call (read) per wave64; anchors are processed in order i (score[i] depends on
-// score[j < i]) and the predecessor loop j = i-1 .. st runs 64 candidates per step, lane l taking
-// j = jtop - l, i.e. lanes in the reference's visiting order. The reference loop is sequential only
-// through three quantities, each turned into a wave-wide prefix scan:
-//   max_f        running maximum of the candidate scores             (max scan)
+// MI355X design: one call (read) per workgroup of two waves; anchors are processed in order i
+// (score[i] depends on score[j < i]) and the predecessor loop j = i-1 .. st runs 64 candidates per
+// step, lane l taking j = jtop - l, i.e. lanes in the reference's visiting order. A producer wave
+// computes the score-independent pair geometry ahead; the consumer wave resolves the reference's
+// loop, which is sequential only through three quantities, each a wave-wide operation:
+//   max_f        running maximum of the candidate scores             (DPP max scan)
 //   n_skip       max(n-1, 0) on an improvement, n+1 on a "targeted" non-improvement
-//                -> compositions of n -> max(n + a, b), closed under composition (pair scan)
+//                -> a reflected walk n = max(N + D, D - min D)      (mbcnt chain + DPP min scan)
 //   break        first lane where n_skip exceeds 25                   (ballot + ctz)
 // "targets[j] == i" is decided by marks from earlier-visited j' (> j) of the same i, which are all
 // visited before any break that could stop j: marks are i+1 stamps in an LDS ring indexed by j.
 // The last 64 anchors (the first step of every i) live in registers, shifted one lane per i with
 // DPP, so most anchors need no memory access at all; older candidates are read from global memory
-// through L2 (sc1 loads) after a periodic vmcnt drain that orders the wave's own stores before them.
+// through L2 (sc1 loads) after a vmcnt drain that orders the wave's own stores before them.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -60,12 +61,10 @@ __device__ __forceinline__ uint64_t dpp_shr_u64(uint64_t v, uint64_t lane0) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-constexpr int32_t kNegB = -(1 << 28);
-
 // anchors are read-only for the whole kernel: the constant address space turns the uniform X[st]
 // reads of the window-start loop into scalar loads (lgkmcnt), so they never wait behind the
 // wave's outstanding score/parent/peak stores (vmcnt)
-typedef const __attribute__((address_space(4))) uint64_t const_u64;  // identity of the n_skip composition scan
+typedef const __attribute__((address_space(4))) uint64_t const_u64;
 
 // wave-wide inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
 __device__ __forceinline__ int32_t scan_max(int32_t v) {
@@ -77,15 +76,6 @@ __device__ __forceinline__ int32_t scan_max(int32_t v) {
   v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xC, 0xF, false));
   return v;
 }
-// (a, b) represents n -> max(n + a, b); earlier lanes apply first: (a1,b1) then (a2,b2) =
-// (a1 + a2, max(b1 + a2, b2)). Identity (0, kNegB).
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void compose_step(int32_t &a, int32_t &b) {
-  const int32_t ua = __builtin_amdgcn_update_dpp(0, a, CTRL, ROWS, 0xF, false);
-  const int32_t ub = __builtin_amdgcn_update_dpp(kNegB, b, CTRL, ROWS, 0xF, false);
-  b = max(ub + a, b);
-  a = ua + a;
-}
 __device__ __forceinline__ int32_t scan_min(int32_t v) {
   v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xF, 0xF, false));
   v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xF, 0xF, false));
@@ -95,20 +85,6 @@ __device__ __forceinline__ int32_t scan_min(int32_t v) {
   v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xC, 0xF, false));
   return v;
 }
-// number of set bits of m in lanes 0..lane (inclusive)
-__device__ __forceinline__ int32_t incl_count(uint64_t m, int lane) {
-  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  return below + (int)((m >> lane) & 1);
-}
-__device__ __forceinline__ void scan_compose(int32_t &a, int32_t &b) {
-  compose_step<0x111, 0xF>(a, b);
-  compose_step<0x112, 0xF>(a, b);
-  compose_step<0x114, 0xF>(a, b);
-  compose_step<0x118, 0xF>(a, b);
-  compose_step<0x142, 0xA>(a, b);
-  compose_step<0x143, 0xC>(a, b);
-}
-
 __device__ __forceinline__ int32_t load_l2(const int32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1 (bypasses L1)
 }
