@@ -55,6 +55,9 @@ constexpr int kIters = 4096;
 #define OP_CMPCND(r) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r) : "v"(k) : "vcc");
 #define OP_CNDS(r) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r) : "v"(k), "s"(sm));
 #define OP_CMP(r) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(r), "v"(k) : "vcc");
+#define OP_MULF_DPP(r) asm volatile("v_mul_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
+#define OP_MULF_ROR(r) asm volatile("v_mul_f32_dpp %0, %0, %1 wave_ror:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
+#define OP_ADDF_DPP(r) asm volatile("v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define OP_ADDF64(r) asm volatile("v_add_f64 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
 
 KERNEL(k_addf, OP_ADDF, 0x3f800000u)
@@ -86,6 +89,9 @@ KERNEL(k_xor, OP_XOR, 1u)
 KERNEL(k_cmpcnd, OP_CMPCND, 1u)
 KERNEL(k_cnds, OP_CNDS, 1u)
 KERNEL(k_cmp, OP_CMP, 1u)
+KERNEL(k_mulf_dpp, OP_MULF_DPP, 0x3f800000u)
+KERNEL(k_mulf_ror, OP_MULF_ROR, 0x3f800000u)
+KERNEL(k_addf_dpp, OP_ADDF_DPP, 0x3f800000u)
 
 typedef void (*KFN)(uint32_t *, unsigned long long *, uint32_t);
 
@@ -102,7 +108,8 @@ int main() {
       {"v_med3_i32", k_med3}, {"v_pk_add_u16", k_pkadd16}, {"v_pk_sub_i16", k_pksub16}, {"v_perm_b32", k_perm},
       {"v_bfe_i32", k_bfe}, {"v_mov_b32", k_mov}, {"v_sub_f32", k_subf}, {"v_fmac_f32", k_fmac},
       {"v_max_f32", k_maxf}, {"v_add_u16", k_addi16}, {"v_lshl_or_b32", k_lshlor},
-      {"cmp+cndmask(vcc)x2", k_cmpcnd}, {"cndmask(sgpr)", k_cnds}, {"v_cmp(vcc)", k_cmp}};
+      {"cmp+cndmask(vcc)x2", k_cmpcnd}, {"cndmask(sgpr)", k_cnds}, {"v_cmp(vcc)", k_cmp},
+      {"v_mul_f32_dpp row_shr", k_mulf_dpp}, {"v_mul_f32_dpp wave_ror", k_mulf_ror}, {"v_add_f32_dpp row_shr", k_addf_dpp}};
   for (auto &k : ks) {
     for (int rep = 0; rep < 2; rep++) {
       CK(hipMemset(clk, 0, 8));
