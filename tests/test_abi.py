@@ -64,3 +64,49 @@ def test_no_device_is_reported_not_faked():
     if n == 0:
         with pytest.raises(gb.GbError):
             gb.set_device(0)
+
+
+def test_chain_rejects_oversized_call_before_touching_the_device():
+    """A call must hold < 2^30 anchors (int32 indices, buffer-store offsets): GB_ERR_ARG, checked
+    before any device work, so this runs without a GPU."""
+    import ctypes
+    import numpy as np
+    from genomicsbench_palisade_amd import lib
+    L = lib()
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    L.gb_chain_batch_create.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.POINTER(vp)]
+    offsets = np.array([0, 1 << 30], np.int64)
+    aq = np.ones(1, np.float32)
+    p4 = np.array([5000, 5000, 500, 1], np.int32)
+    xy = np.zeros(1, np.uint64)  # never read: the size check comes first
+    h = vp()
+    rc = L.gb_chain_batch_create(1, offsets.ctypes.data, aq.ctypes.data, p4.ctypes.data, xy.ctypes.data,
+                                 xy.ctypes.data, ctypes.byref(h))
+    assert rc == -1 and not h.value  # GB_ERR_ARG, no batch
+
+
+def test_pmc_summary_applies_calibrated_read_class_factors(tmp_path):
+    """tools/pmc_summary.py: gather-class kernels keep FETCH_SIZE, stream-class kernels double it
+    (profiles/r01g_pmc_calib.txt), WRITE_SIZE as measured; raw counters are kept."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    cols = ["Kernel_Name", "Counter_Name", "Counter_Value", "Start_Timestamp", "End_Timestamp"]
+    for what, counter, vals in [("fetch", "FETCH_SIZE", (100.0, 10.0)), ("write", "WRITE_SIZE", (7.0, 3.0))]:
+        d = tmp_path / what
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=cols)
+            w.writeheader()
+            w.writerow({"Kernel_Name": "void gbfmi::smem_search<true>(gbfmi::SearchArgs)", "Counter_Name": counter,
+                        "Counter_Value": vals[0], "Start_Timestamp": 0, "End_Timestamp": 1000000})
+            w.writerow({"Kernel_Name": "void gbchain::chain_kernel<0>(gbchain::Args)", "Counter_Name": counter,
+                        "Counter_Value": vals[1], "Start_Timestamp": 0, "End_Timestamp": 2000000})
+    dst = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(tmp_path / "fetch"),
+                    str(tmp_path / "write"), str(dst)], check=True, capture_output=True)
+    d = json.load(open(dst))
+    assert d["smem_search"]["fetch_class"] == "gather" and d["smem_search"]["fetch_bytes"] == 100.0 * 1024
+    assert d["chain_kernel"]["fetch_class"] == "stream" and d["chain_kernel"]["fetch_bytes"] == 2 * 10.0 * 1024
+    assert d["chain_kernel"]["fetch_bytes_raw"] == 10.0 * 1024 and d["chain_kernel"]["write_bytes"] == 3.0 * 1024
