@@ -12,10 +12,10 @@
 //
 // MI355X design: one testcase per wave64; the read is cut into stripes of 64 rows, lane k owns row
 // r0+k and the wave sweeps anti-diagonals (step t: lane k is at column t-k+1). Values move one lane
-// down per step with DPP wave_shr:1 (no LDS round trip); lane 0 takes the row above the stripe and
-// the haplotype base of its column from one uniform LDS record per step, and lane 63 writes the
-// stripe's last row back into the same record (in place: the write index trails the read index by
-// 63 columns). The f32 pass appends testcases that need f64 to a device list; a second kernel
+// down per step with DPP wave_shr:1 (no LDS round trip); lane 0 takes the row above the stripe from
+// one uniform LDS record per step, every lane reads the haplotype code of its own column from an
+// LDS byte array, and lane 63 writes the stripe's last row back into the records (in place: the
+// write index trails the read index by 63 columns). The f32 pass appends testcases that need f64 to a device list; a second kernel
 // recomputes them in f64. Testcases are ordered by descending cost so the dispatcher balances waves.
 #include <hip/hip_runtime.h>
 
