@@ -1,4 +1,8 @@
 #!/bin/bash
+# Chain development run on the GPU box: light profile stamps (GB_CHAIN_PROF=1: grid span, start/end of
+# the longest call) for the longest call alone and for the whole 'large' set, the chain_dp and
+# backtrack GPU parity tests, and tools/chain_probe.py (whole set / longest call / the rest).
+#   gpurun --timeout 900 -- 'bash tools/gpu_chain.sh'
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
