@@ -21,7 +21,19 @@ enum : int {
   kNoStore = 8,   // no targets store
   kNoTail = 16,   // no parent-peak readlane (pkJ = 0)
   kWalkAll = 32,  // always run the n_skip walk (as when another step follows)
+  kOrRed = 64,    // first-window marks from a register OR-reduction instead of the LDS stamps
 };
+
+// wave-wide OR of a 32-bit value, result in lane 63 (row_shr scan, then row broadcasts)
+__device__ __forceinline__ uint32_t or_scan(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+  return v;
+}
 
 template <int V>
 __global__ __launch_bounds__(64) void step_probe(int32_t *target, int n, int iters, int density,
@@ -49,6 +61,14 @@ __global__ __launch_bounds__(64) void step_probe(int32_t *target, int n, int ite
     uint64_t tgm;
     if (V & kNoStamp) {
       tgm = __builtin_amdgcn_ballot_w64((h & 3) == 0);
+    } else if (V & kOrRed) {
+      // bit (jtop - pj) for marking lanes whose parent falls inside this window
+      const int32_t d = jtop - pj;
+      const bool in = ok & (pj >= st) & (d >= 0) & (d < 64);
+      const uint64_t one = in ? 1ull << (d & 63) : 0ull;
+      const uint32_t lo = or_scan((uint32_t)one), hi = or_scan((uint32_t)(one >> 32));
+      tgm = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 63) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32;
     } else {
       S[(ok & (pj >= st)) ? (pj & (kRing - 1)) : kRing + lane] = stamp;
       tgm = __builtin_amdgcn_ballot_w64(S[(jtop - lane) & (kRing - 1)] == stamp);
@@ -120,6 +140,7 @@ int main() {
     if (run<0>("full step", d_t, d_o, density)) return 1;
     if (run<kWalkAll>("full step, walk always", d_t, d_o, density)) return 1;
     if (run<kNoStamp>("- LDS stamp round trip", d_t, d_o, density)) return 1;
+    if (run<kOrRed>("stamps -> register OR-reduction", d_t, d_o, density)) return 1;
     if (run<kNoMax>("- max scan", d_t, d_o, density)) return 1;
     if (run<kNoWalk>("- n_skip walk", d_t, d_o, density)) return 1;
     if (run<kNoStore>("- targets store", d_t, d_o, density)) return 1;
