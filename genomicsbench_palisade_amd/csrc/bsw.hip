@@ -265,7 +265,8 @@ struct LaneArgs {
   int32_t *out6, *cells;
   unsigned long long *total_cells;
   int o_del, e_del, o_ins, e_ins, zdrop;
-  unsigned long long *prof;  // GB_BSW_PROF=1: {wave rows, chunk-columns swept, lane-rows active, cells}
+  unsigned long long *prof;  // GB_BSW_PROF=1: {wave rows, chunk-columns swept, lane-rows active, cells,
+                             //  chunk-columns inside every active lane's band}
   uint32_t tab[10];  // per target code t: biased scores of query codes 0..3 (tab[2t]) and 4 (tab[2t+1])
 };
 
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
   int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
   int ncells = 0;
   bool active = valid && tlen > 0;
-  unsigned long long pr_rows = 0, pr_cols = 0, pr_lrows = 0;
+  unsigned long long pr_rows = 0, pr_cols = 0, pr_lrows = 0, pr_full = 0;
   // target bases: four rows per register; the next four are loaded one group ahead as independent
   // byte loads (clamped in-bounds, never waited on until they are combined four rows later)
   const int tmax = max(tlen - 1, 0);
@@ -365,7 +366,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
       if (c + 1 < NCH) qn = Qs[c + 1][lane];  // prefetch the next chunk's codes
       // skip the chunk when it meets no lane's band
       if (__builtin_amdgcn_ballot_w64(width > 0 && beg < 8 * c + 8 && end > 8 * c) == 0) continue;
-      if (A.prof) pr_cols += 8;
+      if (A.prof) {
+        pr_cols += 8;
+        if (__builtin_amdgcn_ballot_w64(active && (beg > 8 * c || end < 8 * c + 8)) == 0) pr_full += 8;
+      }
       const uint32_t qe = qc & 0x0F0F0F0Fu, qo = (qc >> 4) & 0x0F0F0F0Fu;
       const uint32_t se = __builtin_amdgcn_perm(thi, tlo, qe);  // biased scores, columns 0,2,4,6
       const uint32_t so = __builtin_amdgcn_perm(thi, tlo, qo);  // columns 1,3,5,7
@@ -461,6 +465,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
       atomicAdd(A.prof + 1, pr_cols);
       atomicAdd(A.prof + 2, pr_lrows);
       atomicAdd(A.prof + 3, wc);
+      atomicAdd(A.prof + 4, pr_full);
     }
   }
 }
@@ -652,11 +657,11 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
     const char *pe = getenv("GB_BSW_PROF");
     const bool prof = pe && *pe == '1';
     if (prof) {
-      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 20 * sizeof(unsigned long long)));
-      GB_HIP(hipMemsetAsync(B->d_prof, 0, 20 * sizeof(unsigned long long), B->stream));
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 25 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 25 * sizeof(unsigned long long), B->stream));
     }
     for (int v = 0; v < 5; ++v) {
-      if (prof) L.prof = B->d_prof + 4 * v;
+      if (prof) L.prof = B->d_prof + 5 * v;
       L.first = B->seg[v];
       L.count = B->seg[v + 1] - B->seg[v];
       if (L.count == 0) continue;
@@ -692,16 +697,16 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   B->ran = true;
   if (B->d_prof && getenv("GB_BSW_PROF")) {
-    unsigned long long h[20];
+    unsigned long long h[25];
     GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
     for (int v = 0; v < 5; ++v)
-      if (h[4 * v])
+      if (h[5 * v])
         fprintf(stderr,
                 "[bsw prof] NCH=%d pairs %lld: wave rows %llu, lane-row use %.3f, column use %.3f (cells %llu / "
-                "lane-column slots %llu)\n",
-                4 * (v + 1), (long long)(B->seg[v + 1] - B->seg[v]), h[4 * v], h[4 * v + 2] / (64.0 * h[4 * v]),
-                h[4 * v + 3] / (64.0 * h[4 * v + 1]), h[4 * v + 3], 64 * h[4 * v + 1]);
+                "lane-column slots %llu), chunk-columns inside every band %.3f\n",
+                4 * (v + 1), (long long)(B->seg[v + 1] - B->seg[v]), h[5 * v], h[5 * v + 2] / (64.0 * h[5 * v]),
+                h[5 * v + 3] / (64.0 * h[5 * v + 1]), h[5 * v + 3], 64 * h[5 * v + 1], (double)h[5 * v + 4] / h[5 * v + 1]);
   }
   return GB_OK;
 }
