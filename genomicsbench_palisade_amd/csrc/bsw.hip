@@ -255,7 +255,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void bsw_extend_kernel(Args A)
 // e, f >= 0, and both gap openings clamp at 0), so M is formed as med3(H << 16, H + S, 0); all
 // scores stay below 2^15 (checked on the host), so the 16-bit packing is lossless.
 
-constexpr int kBias = 128;  // score bytes are stored biased (unsigned) for v_perm lookups
+// v_med3_i32(a, b, 0) = max(min(a, b), 0) whenever a >= 0 (LLVM only forms med3 from constant
+// clamps, so it is spelled out)
+__device__ __forceinline__ int med3_0(int a, int b) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 struct LaneArgs {
   const Pair *pairs;
@@ -267,7 +273,7 @@ struct LaneArgs {
   int o_del, e_del, o_ins, e_ins, zdrop;
   unsigned long long *prof;  // GB_BSW_PROF=1: {wave rows, chunk-columns swept, lane-rows active, cells,
                              //  chunk-columns inside every active lane's band}
-  uint32_t tab[10];  // per target code t: biased scores of query codes 0..3 (tab[2t]) and 4 (tab[2t+1])
+  uint32_t tab[10];  // per target code t: score bytes (int8) of query codes 0..3 (tab[2t]) and 4 (tab[2t+1])
 };
 
 template <int NCH>
@@ -371,7 +377,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         if (__builtin_amdgcn_ballot_w64(active && (beg > 8 * c || end < 8 * c + 8)) == 0) pr_full += 8;
       }
       const uint32_t qe = qc & 0x0F0F0F0Fu, qo = (qc >> 4) & 0x0F0F0F0Fu;
-      const uint32_t se = __builtin_amdgcn_perm(thi, tlo, qe);  // biased scores, columns 0,2,4,6
+      const uint32_t se = __builtin_amdgcn_perm(thi, tlo, qe);  // score bytes, columns 0,2,4,6
       const uint32_t so = __builtin_amdgcn_perm(thi, tlo, qo);  // columns 1,3,5,7
       // branch-free: every lane evaluates all 8 columns (one basic block, so the scheduler can overlap
       // column j+1's independent work with column j's f/h1 chain); out-of-band lanes keep their state
@@ -381,9 +387,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         // lane mask of the band, used as a bit-select (kept arithmetic so no branches come back)
         const uint32_t msk = (uint32_t)(j - beg) < (uint32_t)width ? 0xFFFFFFFFu : 0u;
         const uint32_t x = X[j];
-        const uint32_t sb = ((b & 1) ? so : se) >> (8 * (b >> 1)) & 0xFFu;
-        const int y = __builtin_amdgcn_sbfe((int)(x + sb - kBias), 0, 16);  // H + S
-        const int M = max(min((int)(x << 16), y), 0);                        // H ? H + S : 0 (clamped)
+        const int sb = (int)(int8_t)(((b & 1) ? so : se) >> (8 * (b >> 1)));  // score, sign-extended
+        const int y = __builtin_amdgcn_sbfe((int)x + sb, 0, 16);              // H + S
+        const int M = med3_0((int)(x << 16), y);  // H ? H + S : 0 (clamped); x << 16 >= 0 (H < 2^15)
         const int e = (int)(x >> 16);
         const int h = max(max(M, e), f);
         const int en = max(max(e - e_del, M - oe_del), 0);                    // E(i+1,j)
@@ -644,11 +650,11 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
     L.o_ins = B->params.o_ins;
     L.e_ins = B->params.e_ins;
     L.zdrop = B->params.zdrop;
-    for (int t = 0; t < 5; ++t) {  // biased score bytes of row t for query codes 0..3 and 4
+    for (int t = 0; t < 5; ++t) {  // score bytes of row t for query codes 0..3 and 4
       uint32_t lo = 0;
-      for (int q = 0; q < 4; ++q) lo |= (uint32_t)(uint8_t)(B->params.mat[t * 5 + q] + gbbsw::kBias) << (8 * q);
+      for (int q = 0; q < 4; ++q) lo |= (uint32_t)(uint8_t)B->params.mat[t * 5 + q] << (8 * q);
       L.tab[2 * t] = lo;
-      L.tab[2 * t + 1] = (uint32_t)(uint8_t)(B->params.mat[t * 5 + 4] + gbbsw::kBias) | 0x80808000u;
+      L.tab[2 * t + 1] = (uint32_t)(uint8_t)B->params.mat[t * 5 + 4];
     }
     void (*lane_kernels[5])(gbbsw::LaneArgs) = {gbbsw::bsw_lane_kernel<4>, gbbsw::bsw_lane_kernel<8>,
                                                  gbbsw::bsw_lane_kernel<12>, gbbsw::bsw_lane_kernel<16>,
