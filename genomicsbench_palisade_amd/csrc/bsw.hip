@@ -395,11 +395,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         const int en = max(max(e - e_del, M - oe_del), 0);                    // E(i+1,j)
         const int fn = max(max(f - e_ins, M - oe_ins), 0);                    // F(i,j+1)
         const uint32_t xn = ((uint32_t)en << 16) | (uint32_t)h1;             // eh[j] = {H(i,j-1), E}
-        mkey = max(mkey, (int)((((uint32_t)h << 8 | (uint32_t)j) & msk) | ~msk));  // last argmax
         nz[j >> 5] |= (min(xn, 1u) & msk) << (j & 31);
         X[j] = (xn & msk) | (x & ~msk);
         f = (int)(((uint32_t)fn & msk) | ((uint32_t)f & ~msk));
         h1 = (int)(((uint32_t)h & msk) | ((uint32_t)h1 & ~msk));
+        // last argmax over keys (H << 8 | j) built from h1 unmasked: outside the band h1 holds the
+        // last in-band H (or 0 / the row-0 value before it), fixed up once per row below
+        mkey = max(mkey, (int)((uint32_t)h1 << 8 | (uint32_t)j));
       }
     }
     // eh[end] = {h1, 0} (bandedSWA.cpp:217), chunks holding no lane's end skipped
@@ -417,8 +419,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
       }
     }
     if (!active) continue;
-    const int m = mkey < 0 ? 0 : (mkey >> 8);
-    const int mj = mkey < 0 ? -1 : (mkey & 0xFF);
+    // keys past the band end repeat H(end-1) at larger j, so a winner there is column end-1; an
+    // empty band computed nothing (row max 0, bandedSWA.cpp:222)
+    const int m = (mkey < 0 || width == 0) ? 0 : (mkey >> 8);
+    const int mj = mkey < 0 ? -1 : min(mkey & 0xFF, end - 1);
     if ((beg < end ? end : beg) == qlen) {  // bandedSWA.cpp:218-221
       max_ie = gscore > h1 ? max_ie : i;
       gscore = gscore > h1 ? gscore : h1;
