@@ -246,9 +246,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void bsw_extend_kernel(Args A)
 // ------------------------------------------------------------------------------------------------
 // Pair-per-lane kernel (the reference's own inter-pair SIMD shape, getScores16): 64 pairs per wave,
 // each lane runs scalarBandedSWA for its pair. The lane's eh[0..qlen] lives in VGPRs, one register
-// per column packing h (bits 0-15) and e (bits 16-31), so every column index is a compile-time
+// per column packing e (bits 0-15) and h (bits 16-31: H + S is one SDWA add of the high word and
+// the sign-extended score byte, H << 16 one AND), so every column index is a compile-time
 // constant: columns are swept in lockstep over the union of the lanes' bands, each lane's own band
-// [beg, end) selected by the EXEC mask, 8-column chunks outside every band skipped by a uniform
+// [beg, end) selected by a bit-select mask, 8-column chunks outside every band skipped by a uniform
 // branch. Pairs are grouped by query length (NCH chunks of 8 columns hold eh[0..8*NCH-1]) and
 // sorted by target length so the 64 lanes of a wave run rows in near lockstep.
 // Exactness notes: M = H ? H + S : 0 only matters through max(M, 0) (h = max(M, e, f) with
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
   }
 #pragma unroll
   for (int j = 0; j < NCOL; ++j)
-    X[j] = j == 0 ? (uint32_t)h0 : (j <= qlen ? (uint32_t)max(v1 - (j - 1) * e_ins, 0) : 0u);
+    X[j] = (j == 0 ? (uint32_t)h0 : (j <= qlen ? (uint32_t)max(v1 - (j - 1) * e_ins, 0) : 0u)) << 16;
 
   int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
   int ncells = 0;
@@ -391,13 +392,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         const uint32_t msk = (uint32_t)(j - beg) < (uint32_t)width ? 0xFFFFFFFFu : 0u;
         const uint32_t x = X[j];
         const int sb = (int)(int8_t)(((b & 1) ? so : se) >> (8 * (b >> 1)));  // score, sign-extended
-        const int y = __builtin_amdgcn_sbfe((int)x + sb, 0, 16);              // H + S
-        const int M = med3_0((int)(x << 16), y);  // H ? H + S : 0 (clamped); x << 16 >= 0 (H < 2^15)
-        const int e = (int)(x >> 16);
+        const int y = (int)(x >> 16) + sb;                                    // H + S
+        const int M = med3_0((int)(x & 0xFFFF0000u), y);  // H ? H + S : 0 (clamped); H << 16 >= 0 (H < 2^15)
+        const int e = (int)(x & 0xFFFFu);
         const int h = max(max(M, e), f);
         const int en = max(max(e - e_del, M - oe_del), 0);                    // E(i+1,j)
         const int fn = max(max(f - e_ins, M - oe_ins), 0);                    // F(i,j+1)
-        const uint32_t xn = ((uint32_t)en << 16) | (uint32_t)h1;             // eh[j] = {H(i,j-1), E}
+        const uint32_t xn = ((uint32_t)h1 << 16) | (uint32_t)en;             // eh[j] = {H(i,j-1), E}
         nz[j >> 5] |= (min(xn, 1u) & msk) << (j & 31);
         X[j] = (xn & msk) | (x & ~msk);
         f = (int)(((uint32_t)fn & msk) | ((uint32_t)f & ~msk));
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
       for (int b = 0; b < 8; ++b) {
         const int j = 8 * c + b;
         if (wend && end == j) {
-          X[j] = (uint32_t)h1;
+          X[j] = (uint32_t)h1 << 16;
           nz[j >> 5] = (nz[j >> 5] & ~(1u << (j & 31))) | (min((uint32_t)h1, 1u) << (j & 31));
         }
       }
