@@ -328,25 +328,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
   int ncells = 0;
   bool active = valid && tlen > 0;
   unsigned long long pr_rows = 0, pr_cols = 0, pr_lrows = 0, pr_full = 0;
-  // target bases: four rows per register; the next four are loaded one group ahead as independent
-  // byte loads (clamped in-bounds, never waited on until they are combined four rows later)
+  // target bases: the next row's byte is loaded one row ahead (clamped in-bounds) into one register;
+  // a row of sweeping hides its latency, and the 256-VGPR variants keep it out of scratch (a
+  // four-row prefetch group spilled there and waited on each load)
   const int tmax = max(tlen - 1, 0);
-  uint32_t tcur = 0, tn[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b) tcur |= (uint32_t)tgt[min(b, tmax)] << (8 * b);
-#pragma unroll
-  for (int b = 0; b < 4; ++b) tn[b] = tgt[min(4 + b, tmax)];
+  uint32_t tnext = tgt[0];
+  // per-lane constants used once per row (target pointer, last row, band width) live in LDS and are
+  // re-read each row: in the 256-VGPR variants they were spilled to scratch instead, and a scratch
+  // reload's vmcnt wait also waited for the row-ahead target load
+  __shared__ uint32_t Pc[4][64];
+  Pc[0][lane] = (uint32_t)(uintptr_t)tgt;
+  Pc[1][lane] = (uint32_t)((uint64_t)(uintptr_t)tgt >> 32);
+  Pc[2][lane] = (uint32_t)tmax;
+  Pc[3][lane] = (uint32_t)w;
+  typedef volatile __attribute__((address_space(3))) uint32_t lds_u32;  // ds_read, never flat
 
 #pragma unroll 1
   for (int i = 0;; ++i) {
     if (i >= tlen) active = false;
     if (__builtin_amdgcn_ballot_w64(active) == 0) break;
-    if (i > 0 && (i & 3) == 0) {
-      tcur = tn[0] | tn[1] << 8 | tn[2] << 16 | tn[3] << 24;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) tn[b] = tgt[min(i + 4 + b, tmax)];
+    const uint32_t tb = min(tnext, 4u);
+    const int wr = (int)*(lds_u32 *)&Pc[3][lane];
+    {
+      // a global (not flat) pointer: a flat load would also count on lgkmcnt and the chunk loop's LDS
+      // waits would wait for it
+      typedef const __attribute__((address_space(1))) uint8_t glb_u8;
+      glb_u8 *tg = (glb_u8 *)(uintptr_t)((uint64_t) * (lds_u32 *)&Pc[1][lane] << 32 | *(lds_u32 *)&Pc[0][lane]);
+      tnext = tg[min(i + 1, (int)*(lds_u32 *)&Pc[2][lane])];
     }
-    const uint32_t tb = min((tcur >> (8 * (i & 3))) & 0xFFu, 4u);
     uint32_t tlo = A.tab[8], thi = A.tab[9];  // per-lane row of the score table (select chain, no scratch)
 #pragma unroll
     for (int t = 3; t >= 0; --t)
@@ -355,8 +364,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         thi = A.tab[2 * t + 1];
       }
     // band (bandedSWA.cpp:180-182)
-    if (beg < i - w) beg = i - w;
-    if (end > i + w + 1) end = i + w + 1;
+    if (beg < i - wr) beg = i - wr;
+    if (end > i + wr + 1) end = i + wr + 1;
     if (end > qlen) end = qlen;
     const int width = active ? max(end - beg, 0) : 0;
     ncells += width;
