@@ -422,9 +422,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
     }
     // eh[end] = {h1, 0} (bandedSWA.cpp:217), chunks holding no lane's end skipped
     const bool wend = active && end < NCOL;
+    // chunks holding some lane's end: one wave OR of one-hot chunk bits (DPP row shifts + row
+    // broadcasts, lane 63 holds the result), then scalar bit tests instead of a ballot per chunk
+    uint32_t endm = wend ? 1u << (end >> 3) : 0u;
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x111, 0xF, 0xF, false);
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x112, 0xF, 0xF, false);
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x114, 0xF, 0xF, false);
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x118, 0xF, 0xF, false);
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x142, 0xA, 0xF, false);
+    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x143, 0xC, 0xF, false);
+    endm = (uint32_t)__builtin_amdgcn_readlane((int)endm, 63);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      if (__builtin_amdgcn_ballot_w64(wend && (end >> 3) == c) == 0) continue;
+      if (((endm >> c) & 1u) == 0) continue;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const int j = 8 * c + b;
