@@ -264,6 +264,17 @@ __device__ __forceinline__ int med3_0(int a, int b) {
   return r;
 }
 
+// wave-wide OR, result uniform (DPP row shifts and row broadcasts leave it in lane 63)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 struct LaneArgs {
   const Pair *pairs;
   const uint32_t *order;
@@ -379,12 +390,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
 #pragma unroll
     for (int q = 0; q < NW; ++q) nz[q] = 0;
     uint32_t qn = Qs[0][lane];
+    // chunks meeting some lane's band: the OR of every lane's chunk range [beg >> 3, (end - 1) >> 3]
+    const uint32_t swm = wave_or(width > 0 ? (2u << ((end - 1) >> 3)) - (1u << (beg >> 3)) : 0u);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const uint32_t qc = qn;
       if (c + 1 < NCH) qn = Qs[c + 1][lane];  // prefetch the next chunk's codes
       // skip the chunk when it meets no lane's band
-      if (__builtin_amdgcn_ballot_w64(width > 0 && beg < 8 * c + 8 && end > 8 * c) == 0) continue;
+      if (((swm >> c) & 1u) == 0) continue;
       if (A.prof) {
         pr_cols += 8;
         if (__builtin_amdgcn_ballot_w64(active && (beg > 8 * c || end < 8 * c + 8)) == 0) pr_full += 8;
@@ -424,14 +437,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
     const bool wend = active && end < NCOL;
     // chunks holding some lane's end: one wave OR of one-hot chunk bits (DPP row shifts + row
     // broadcasts, lane 63 holds the result), then scalar bit tests instead of a ballot per chunk
-    uint32_t endm = wend ? 1u << (end >> 3) : 0u;
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x111, 0xF, 0xF, false);
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x112, 0xF, 0xF, false);
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x114, 0xF, 0xF, false);
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x118, 0xF, 0xF, false);
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x142, 0xA, 0xF, false);
-    endm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)endm, 0x143, 0xC, 0xF, false);
-    endm = (uint32_t)__builtin_amdgcn_readlane((int)endm, 63);
+    const uint32_t endm = wave_or(wend ? 1u << (end >> 3) : 0u);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (((endm >> c) & 1u) == 0) continue;
