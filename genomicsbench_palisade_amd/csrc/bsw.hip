@@ -540,6 +540,7 @@ struct gb_bsw_batch {
   uint8_t *d_tgt = nullptr, *d_qry = nullptr;
   int32_t *d_out6 = nullptr, *d_cells = nullptr;
   unsigned long long *d_total = nullptr;  // [0] total cells, [1] work counter
+  size_t cap_n = 0, cap_tgt = 0, cap_qry = 0;  // allocated capacities (cached workspaces are refilled)
   bool ran = false;
 };
 
@@ -579,11 +580,44 @@ int gb_bsw_batch_destroy(gb_bsw_batch *B) {
   return GB_OK;
 }
 
-int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, int64_t n,
-                        const uint8_t *ref, int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes,
-                        gb_bsw_batch **out) {
-  GB_ARG(out && params && n >= 0 && (n == 0 || pairs), "gb_bsw_batch_create: bad arguments");
-  *out = nullptr;
+}  // extern "C"
+
+namespace {
+
+int bsw_batch_new(gb_bsw_batch **out) {
+  auto *B = new gb_bsw_batch();
+  hipError_t e = hipGetDevice(&B->device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&B->num_cus, hipDeviceAttributeMultiprocessorCount, B->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
+  for (auto &ev : B->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e == hipSuccess) e = hipMalloc(&B->d_total, 2 * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    gb::set_error("gb_bsw_batch_create: %s", hipGetErrorString(e));
+    gb_bsw_batch_destroy(B);
+    return GB_ERR_HIP;
+  }
+  *out = B;
+  return GB_OK;
+}
+
+// grow-only device buffer
+template <typename T>
+int bsw_reserve(T **p, size_t &cap, size_t want) {
+  if (want <= cap) return GB_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  cap = 0;
+  GB_HIP(hipMalloc(p, want * sizeof(T)));
+  cap = want;
+  return GB_OK;
+}
+
+// Validate, classify and order the pairs (launch plan), then upload them and the sequence buffers
+// into B (buffers grow when too small).
+int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpair *pairs, int64_t n,
+                   const uint8_t *ref, int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes) {
+  GB_ARG(params && n >= 0 && (n == 0 || pairs), "gb_bsw_batch_create: bad arguments");
   GB_ARG(n < (1ll << 32) - 1, "gb_bsw_batch_create: too many pairs");
   GB_ARG(params->e_del > 0 && params->e_ins > 0, "gb_bsw_batch_create: gap extension must be > 0");
   GB_ARG(ref_bytes >= 0 && qer_bytes >= 0 && (ref_bytes == 0 || ref) && (qer_bytes == 0 || qer),
@@ -635,33 +669,45 @@ int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, in
     }
     for (int64_t p = 0; p < n; ++p) order[cnt[key(p)]++] = (uint32_t)p;
   }
-  auto *B = new gb_bsw_batch();
   for (int v = 0; v <= gb_bsw_batch::kVariants; ++v) B->seg[v] = 0;
   for (int64_t p = 0; p < n; ++p) B->seg[var[p] + 1]++;
   for (int v = 0; v < gb_bsw_batch::kVariants; ++v) B->seg[v + 1] += B->seg[v];
   B->params = *params;
   B->n = n;
-  hipError_t e = hipGetDevice(&B->device);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&B->num_cus, hipDeviceAttributeMultiprocessorCount, B->device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
-  for (auto &ev : B->ev)
-    if (e == hipSuccess) e = hipEventCreate(&ev);
+  B->ran = false;
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
-  if (e == hipSuccess) e = hipMalloc(&B->d_pairs, nn * sizeof(gbbsw::Pair));
-  if (e == hipSuccess) e = hipMalloc(&B->d_order, nn * sizeof(uint32_t));
-  if (e == hipSuccess && n) e = hipMemcpy(B->d_order, order.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&B->d_tgt, (size_t)std::max<int64_t>(ref_bytes, 1));
-  if (e == hipSuccess) e = hipMalloc(&B->d_qry, (size_t)std::max<int64_t>(qer_bytes, 1));
-  if (e == hipSuccess) e = hipMalloc(&B->d_out6, nn * 6 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_cells, nn * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_total, 2 * sizeof(unsigned long long));
-  if (e == hipSuccess && n) e = hipMemcpy(B->d_pairs, P.data(), (size_t)n * sizeof(gbbsw::Pair), hipMemcpyHostToDevice);
-  if (e == hipSuccess && ref_bytes) e = hipMemcpy(B->d_tgt, ref, (size_t)ref_bytes, hipMemcpyHostToDevice);
-  if (e == hipSuccess && qer_bytes) e = hipMemcpy(B->d_qry, qer, (size_t)qer_bytes, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    gb::set_error("gb_bsw_batch_create: %s", hipGetErrorString(e));
+  size_t cap_pairs = B->cap_n, cap_order = B->cap_n, cap_out = B->cap_n * 6, cap_cells = B->cap_n;
+  int st = bsw_reserve(&B->d_pairs, cap_pairs, nn);
+  if (!st) st = bsw_reserve(&B->d_order, cap_order, nn);
+  if (!st) st = bsw_reserve(&B->d_out6, cap_out, nn * 6);
+  if (!st) st = bsw_reserve(&B->d_cells, cap_cells, nn);
+  if (st) return st;
+  B->cap_n = std::max(B->cap_n, nn);
+  if ((st = bsw_reserve(&B->d_tgt, B->cap_tgt, (size_t)std::max<int64_t>(ref_bytes, 1)))) return st;
+  if ((st = bsw_reserve(&B->d_qry, B->cap_qry, (size_t)std::max<int64_t>(qer_bytes, 1)))) return st;
+  if (n) GB_HIP(hipMemcpyAsync(B->d_order, order.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, B->stream));
+  if (n) GB_HIP(hipMemcpyAsync(B->d_pairs, P.data(), (size_t)n * sizeof(gbbsw::Pair), hipMemcpyHostToDevice, B->stream));
+  if (ref_bytes) GB_HIP(hipMemcpyAsync(B->d_tgt, ref, (size_t)ref_bytes, hipMemcpyHostToDevice, B->stream));
+  if (qer_bytes) GB_HIP(hipMemcpyAsync(B->d_qry, qer, (size_t)qer_bytes, hipMemcpyHostToDevice, B->stream));
+  GB_HIP(hipStreamSynchronize(B->stream));  // the host vectors die on return
+  return GB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, int64_t n,
+                        const uint8_t *ref, int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes,
+                        gb_bsw_batch **out) {
+  GB_ARG(out, "gb_bsw_batch_create: null out");
+  *out = nullptr;
+  gb_bsw_batch *B = nullptr;
+  int st = bsw_batch_new(&B);
+  if (st) return st;
+  if ((st = bsw_batch_fill(B, params, pairs, n, ref, ref_bytes, qer, qer_bytes))) {
     gb_bsw_batch_destroy(B);
-    return GB_ERR_HIP;
+    return st;
   }
   *out = B;
   return GB_OK;
@@ -812,15 +858,31 @@ int gb_bsw_batch_timing(gb_bsw_batch *B, float *kernel_ms) {
   return GB_OK;
 }
 
+int gb_bsw_get_scores16_ex(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
+                           int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes, int64_t *total_cells) {
+  // one cached batch per (host thread, device): the reference calls getScores16 once per batch of
+  // 512 pairs (main_banded.cpp:896-909), so streams, events and buffers are reused across calls.
+  // Never freed (freeing at thread exit could run after the HIP runtime is torn down).
+  thread_local std::vector<std::pair<int, gb_bsw_batch *>> ws;
+  int dev = 0;
+  GB_HIP(hipGetDevice(&dev));
+  gb_bsw_batch *B = nullptr;
+  for (auto &w : ws)
+    if (w.first == dev) B = w.second;
+  int st = GB_OK;
+  if (!B) {
+    if ((st = bsw_batch_new(&B))) return st;
+    ws.emplace_back(dev, B);
+  }
+  if ((st = bsw_batch_fill(B, params, pairs, n, ref, ref_bytes, qer, qer_bytes))) return st;
+  st = gb_bsw_batch_run(B);
+  if (!st) st = gb_bsw_batch_results(B, pairs, nullptr, nullptr, total_cells);
+  return st;
+}
+
 int gb_bsw_get_scores16(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
                         int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes) {
-  gb_bsw_batch *B = nullptr;
-  int st = gb_bsw_batch_create(params, pairs, n, ref, ref_bytes, qer, qer_bytes, &B);
-  if (st) return st;
-  st = gb_bsw_batch_run(B);
-  if (!st) st = gb_bsw_batch_results(B, pairs, nullptr, nullptr, nullptr);
-  gb_bsw_batch_destroy(B);
-  return st;
+  return gb_bsw_get_scores16_ex(params, pairs, n, ref, ref_bytes, qer, qer_bytes, nullptr);
 }
 
 }  // extern "C"

@@ -20,11 +20,16 @@ static void die(const char *what, int st) {
   abort();
 }
 
+// HIP's current device is per host thread and the reference calls getScores16 from an OpenMP
+// team (main_banded.cpp:896-909): every calling thread selects GB_DEVICE once (thread_local flag).
 static void ensure_device() {
-  static bool done = false;
+  static const int dev = [] {
+    const char *d = getenv("GB_DEVICE");
+    return d ? atoi(d) : 0;
+  }();
+  thread_local bool done = false;
   if (done) return;
-  const char *d = getenv("GB_DEVICE");
-  const int st = gb_set_device(d ? atoi(d) : 0);
+  const int st = gb_set_device(dev);
   if (st) die("gb_set_device", st);
   done = true;
 }
@@ -63,14 +68,10 @@ void BandedPairWiseSW::getScores16(SeqPair *pairArray, uint8_t *seqBufRef, uint8
   const auto t0 = std::chrono::steady_clock::now();
   gb_bsw_params p = p_;
   p.w = w;
-  gb_bsw_batch *b = nullptr;
-  int st = gb_bsw_batch_create(&p, gbp(pairArray), numPairs, seqBufRef, span_end(pairArray, numPairs, true), seqBufQer,
-                               span_end(pairArray, numPairs, false), &b);
-  if (st) die("gb_bsw_batch_create", st);
-  if ((st = gb_bsw_batch_run(b))) die("gb_bsw_batch_run", st);
   int64_t cells = 0;
-  if ((st = gb_bsw_batch_results(b, gbp(pairArray), nullptr, nullptr, &cells))) die("gb_bsw_batch_results", st);
-  gb_bsw_batch_destroy(b);
+  const int st = gb_bsw_get_scores16_ex(&p, gbp(pairArray), numPairs, seqBufRef, span_end(pairArray, numPairs, true),
+                                        seqBufQer, span_end(pairArray, numPairs, false), &cells);
+  if (st) die("gb_bsw_get_scores16", st);
   SW_cells += (uint64_t)cells;
   ticks_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }

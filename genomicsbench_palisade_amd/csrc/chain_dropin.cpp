@@ -14,14 +14,21 @@ static void die(const char *what, int st) {
   abort();
 }
 
-void host_chain_kernel(std::vector<call_t> &arg, std::vector<return_t> &ret, int /*numThreads*/) {
-  static bool dev_set = false;
-  if (!dev_set) {
+// HIP's current device is per host thread: every calling thread selects GB_DEVICE once.
+static void ensure_device() {
+  static const int dev = [] {
     const char *d = getenv("GB_DEVICE");
-    int st = gb_set_device(d ? atoi(d) : 0);
-    if (st) die("gb_set_device", st);
-    dev_set = true;
-  }
+    return d ? atoi(d) : 0;
+  }();
+  thread_local bool done = false;
+  if (done) return;
+  const int st = gb_set_device(dev);
+  if (st) die("gb_set_device", st);
+  done = true;
+}
+
+void host_chain_kernel(std::vector<call_t> &arg, std::vector<return_t> &ret, int /*numThreads*/) {
+  ensure_device();
   const int64_t nc = (int64_t)arg.size();
   std::vector<int64_t> off((size_t)nc + 1, 0);
   for (int64_t c = 0; c < nc; c++) off[c + 1] = off[c] + (int64_t)arg[c].anchors.size();

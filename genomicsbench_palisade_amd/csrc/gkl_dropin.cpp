@@ -15,16 +15,29 @@ static void die(const char *what, int st) {
   abort();
 }
 
-void initPairHMM() {
-  const char *dev = getenv("GB_DEVICE");
-  int st = gb_set_device(dev ? atoi(dev) : 0);
+// HIP's current device is per host thread: every calling thread selects GB_DEVICE once (the
+// reference's callers may run computelikelihoods* from threads other than initPairHMM's).
+static void ensure_device() {
+  static const int dev = [] {
+    const char *d = getenv("GB_DEVICE");
+    return d ? atoi(d) : 0;
+  }();
+  thread_local bool done = false;
+  if (done) return;
+  const int st = gb_set_device(dev);
   if (st) die("gb_set_device", st);
-  st = gb_phmm_init();
+  done = true;
+}
+
+void initPairHMM() {
+  ensure_device();
+  int st = gb_phmm_init();
   if (st) die("gb_phmm_init", st);
   printf("MI355X (gfx950) PairHMM initialized\n");
 }
 
 void computelikelihoodsboth(testcase *testcases, double *expected_results, int batch_size) {
+  ensure_device();
   int st = gb_phmm_compute(reinterpret_cast<const gb_testcase *>(testcases), batch_size,
                            expected_results, nullptr, nullptr, nullptr);
   if (st) die("gb_phmm_compute", st);
@@ -35,6 +48,7 @@ void computelikelihoodsboth(testcase *testcases, double *expected_results, int b
 }
 
 void computelikelihoodsfloat(testcase *testcases, float *expected_result) {
+  ensure_device();
   // f32 probability only (no f64 fallback), as IntelPairHmmCSource.cpp:89-99
   float rf = 0.f;
   double res = 0.0;
@@ -45,6 +59,7 @@ void computelikelihoodsfloat(testcase *testcases, float *expected_result) {
 }
 
 void computelikelihoodsdouble(testcase *testcases, double *expected_result) {
+  ensure_device();
   // f64 probability (IntelPairHmmCSource.cpp:103-115): force the f64 pass via the raw value.
   float rf = 0.f;
   double rd = 0.0, res = 0.0;

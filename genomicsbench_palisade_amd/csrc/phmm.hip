@@ -34,7 +34,9 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kMaxHaplen = 4096;
+// Longest haplotype: the f64 kernel's LDS (16-B boundary record + 1 code byte per column, plus
+// kBndPad + kWave pad columns) must fit the 160 KB of one CU.
+constexpr int kMaxHaplen = 9400;
 constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_stripe reads)
 constexpr int kQualTab = 128;
 constexpr int kM2M = ((127 * 128) >> 1) + 128;  // set_mm_prob indices for quals < 128
@@ -282,8 +284,16 @@ __device__ __forceinline__ void load_row(const uint8_t *__restrict__ rbase, int 
   dmis = tab.div3[q];
 }
 
-// One testcase per 64-lane workgroup. f64 pass: `f64_list`/`f64_count` remap blockIdx to the
-// testcases the f32 pass flagged (null list = every testcase).
+// One testcase per 64-lane workgroup (f32 pass: blockIdx = testcase; f64 pass over every testcase
+// when `f64_list` is null). The f64 fallback pass is persistent instead: a grid sized to the
+// resident capacity takes the testcases the f32 pass flagged from `f64_list` through the counter
+// f64_count[1], so no workgroup is launched for the ~70 % of testcases that need no fallback.
+template <typename T, bool kF64Pass>
+__device__ __forceinline__ void phmm_testcase(int w, const TcDesc *__restrict__ descs,
+                                              const uint8_t *__restrict__ pool, const DevTab<T> &tab,
+                                              T *__restrict__ raw_out, int *__restrict__ f64_list,
+                                              int *__restrict__ f64_count, uint8_t *smem_raw);
+
 template <typename T, bool kF64Pass>
 __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ descs,
                                                     const uint8_t *__restrict__ pool,
@@ -291,14 +301,28 @@ __global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ de
                                                     int *__restrict__ f64_list,
                                                     int *__restrict__ f64_count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-
-  int w = blockIdx.x;
   if constexpr (kF64Pass) {
-    if (f64_count) {
-      if (w >= *f64_count) return;
-      w = f64_list[w];
+    if (f64_list) {
+      const int total = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f64_count, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT));
+      while (true) {
+        int k = 0;
+        if (threadIdx.x == 0) k = atomicAdd(f64_count + 1, 1);
+        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+        if (k >= total) return;
+        phmm_testcase<T, true>(f64_list[k], descs, pool, tab, raw_out, nullptr, nullptr, smem_raw);
+        __syncthreads();  // the next testcase re-initialises the LDS records
+      }
     }
   }
+  phmm_testcase<T, kF64Pass>(blockIdx.x, descs, pool, tab, raw_out, f64_list, f64_count, smem_raw);
+}
+
+template <typename T, bool kF64Pass>
+__device__ __forceinline__ void phmm_testcase(int w, const TcDesc *__restrict__ descs,
+                                              const uint8_t *__restrict__ pool, const DevTab<T> &tab,
+                                              T *__restrict__ raw_out, int *__restrict__ f64_list,
+                                              int *__restrict__ f64_count, uint8_t *smem_raw) {
   const TcDesc desc = descs[w];
   const int R = (int)(desc.dims & 0xffff);
   const int C = (int)(desc.dims >> 16);
@@ -495,7 +519,9 @@ struct gb_phmm_batch {
   double *d_rd = nullptr;
   double *d_out = nullptr;
   int *d_list = nullptr;
-  int *d_count = nullptr;
+  int *d_count = nullptr;  // [0] f64 fallbacks flagged by the f32 pass, [1] f64 work counter
+  size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
+  int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
   bool ran = false;
   bool force_f64 = false;
 };
@@ -507,14 +533,13 @@ int gb_phmm_init(void) {
   return get_device_tables(&t);
 }
 
-int gb_phmm_batch_create(const gb_testcase *tcs, int n, gb_phmm_batch **out) {
-  GB_ARG(out, "gb_phmm_batch_create: null out");
-  GB_ARG(n >= 0 && (n == 0 || tcs), "gb_phmm_batch_create: bad testcase array (n=%d)", n);
-  *out = nullptr;
-  DeviceTables *tabs = nullptr;
-  int st = get_device_tables(&tabs);
-  if (st) return st;
+}  // extern "C"
 
+namespace {
+
+// Pack the testcases (deduplicated reads/haplotypes, LPT order) and upload them into b, growing its
+// device buffers when they are too small. b's stream/events exist already.
+int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
   // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once.
   std::vector<uint8_t> pool;
@@ -577,36 +602,91 @@ int gb_phmm_batch_create(const gb_testcase *tcs, int n, gb_phmm_batch **out) {
   if (pool.empty()) pool.resize(4);
   pool.resize((pool.size() + 15) & ~size_t(15));
 
-  auto *b = new gb_phmm_batch();
-  b->tabs = tabs;
+  const size_t nn = std::max(n, 1);
+  if (nn > b->cap_n) {
+    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_list})
+      (void)hipFree(p);
+    b->d_desc = nullptr;
+    b->d_rf = nullptr;
+    b->d_rd = b->d_out = nullptr;
+    b->d_list = nullptr;
+    b->cap_n = 0;
+    GB_HIP(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
+    GB_HIP(hipMalloc(&b->d_rf, sizeof(float) * nn));
+    GB_HIP(hipMalloc(&b->d_rd, sizeof(double) * nn));
+    GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
+    GB_HIP(hipMalloc(&b->d_list, sizeof(int) * nn));
+    b->cap_n = nn;
+  }
+  if (pool.size() > b->cap_pool) {
+    (void)hipFree(b->d_pool);
+    b->d_pool = nullptr;
+    b->cap_pool = 0;
+    GB_HIP(hipMalloc(&b->d_pool, pool.size()));
+    b->cap_pool = pool.size();
+  }
+  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 2 * sizeof(int)));
+  if (n) GB_HIP(hipMemcpyAsync(b->d_desc, sorted.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
+  GB_HIP(hipMemcpyAsync(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice, b->stream));
+  GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
   b->n = n;
   b->max_haplen = max_h;
   b->cells = cells;
-  auto fail = [&](int code) {
+  b->ran = false;
+  return GB_OK;
+}
+
+int batch_new(DeviceTables *tabs, gb_phmm_batch **out) {
+  auto *b = new gb_phmm_batch();
+  b->tabs = tabs;
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, tabs->device) == hipSuccess) cus = prop.multiProcessorCount;
+  b->f64_grid = cus * 16;
+  hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+  for (auto &ev : b->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e != hipSuccess) {
+    gb::set_error("gb_phmm_batch_create: %s", hipGetErrorString(e));
     gb_phmm_batch_destroy(b);
-    return code;
-  };
-#define GB_HIPB(expr)                                                                       \
-  do {                                                                                      \
-    hipError_t _e = (expr);                                                                 \
-    if (_e != hipSuccess) {                                                                 \
-      gb::set_error("%s failed: %s", #expr, hipGetErrorString(_e));                         \
-      return fail(GB_ERR_HIP);                                                              \
-    }                                                                                       \
-  } while (0)
-  GB_HIPB(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-  for (auto &e : b->ev) GB_HIPB(hipEventCreate(&e));
-  const size_t nn = std::max(n, 1);
-  GB_HIPB(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
-  GB_HIPB(hipMalloc(&b->d_pool, pool.size()));
-  GB_HIPB(hipMalloc(&b->d_rf, sizeof(float) * nn));
-  GB_HIPB(hipMalloc(&b->d_rd, sizeof(double) * nn));
-  GB_HIPB(hipMalloc(&b->d_out, sizeof(double) * nn));
-  GB_HIPB(hipMalloc(&b->d_list, sizeof(int) * nn));
-  GB_HIPB(hipMalloc(&b->d_count, sizeof(int)));
-  if (n) GB_HIPB(hipMemcpy(b->d_desc, sorted.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice));
-  GB_HIPB(hipMemcpy(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice));
-#undef GB_HIPB
+    return GB_ERR_HIP;
+  }
+  *out = b;
+  return GB_OK;
+}
+
+// gb_phmm_compute's workspace: one batch per (host thread, device), refilled on every call so the
+// reference's once-per-batch computelikelihoodsboth does not create streams, events and buffers
+// each time. Kept for the life of the thread's process (never freed: freeing at thread exit could
+// run after the HIP runtime is torn down).
+gb_phmm_batch *thread_workspace(DeviceTables *tabs, int *st) {
+  thread_local std::unordered_map<int, gb_phmm_batch *> ws;
+  auto it = ws.find(tabs->device);
+  if (it != ws.end()) return it->second;
+  gb_phmm_batch *b = nullptr;
+  *st = batch_new(tabs, &b);
+  if (*st) return nullptr;
+  ws[tabs->device] = b;
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gb_phmm_batch_create(const gb_testcase *tcs, int n, gb_phmm_batch **out) {
+  GB_ARG(out, "gb_phmm_batch_create: null out");
+  GB_ARG(n >= 0 && (n == 0 || tcs), "gb_phmm_batch_create: bad testcase array (n=%d)", n);
+  *out = nullptr;
+  DeviceTables *tabs = nullptr;
+  int st = get_device_tables(&tabs);
+  if (st) return st;
+  gb_phmm_batch *b = nullptr;
+  if ((st = batch_new(tabs, &b))) return st;
+  if ((st = batch_fill(b, tcs, n))) {
+    gb_phmm_batch_destroy(b);
+    return st;
+  }
   *out = b;
   return GB_OK;
 }
@@ -617,7 +697,7 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipSetDevice(t->device));
   const int n = b->n;
   GB_HIP(hipEventRecord(b->ev[0], b->stream));
-  GB_HIP(hipMemsetAsync(b->d_count, 0, sizeof(int), b->stream));
+  GB_HIP(hipMemsetAsync(b->d_count, 0, 2 * sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
     const size_t span = (size_t)(b->max_haplen + kBndPad + kWave);  // records and code bytes
@@ -631,7 +711,9 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
-    hipLaunchKernelGGL(f64k, dim3(n), dim3(kWave), lds_d, b->stream, b->d_desc, b->d_pool,
+    // f64 fallback: persistent grid over the flagged list (every testcase when forced)
+    const int g64 = b->force_f64 ? n : std::min(n, b->f64_grid);
+    hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_desc, b->d_pool,
                        dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
                        b->force_f64 ? nullptr : b->d_list, b->force_f64 ? nullptr : b->d_count);
     GB_HIP(hipGetLastError());
@@ -730,27 +812,33 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
 
 int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f, double *raw_d,
                     uint8_t *used_double) {
-  GB_ARG(n >= 0, "gb_phmm_compute: n < 0");
+  GB_ARG(n >= 0 && (n == 0 || tcs), "gb_phmm_compute: bad testcase array (n=%d)", n);
   if (n == 0) return GB_OK;
-  gb_phmm_batch *b = nullptr;
-  int st = gb_phmm_batch_create(tcs, n, &b);
+  DeviceTables *tabs = nullptr;
+  int st = get_device_tables(&tabs);
   if (st) return st;
+  gb_phmm_batch *b = thread_workspace(tabs, &st);
+  if (!b) return st;
+  b->force_f64 = false;
+  if ((st = batch_fill(b, tcs, n))) return st;
   st = gb_phmm_batch_run(b);
   if (!st) st = gb_phmm_batch_results(b, results, raw_f, raw_d, used_double, nullptr);
-  gb_phmm_batch_destroy(b);
   return st;
 }
 
 int gb_phmm_compute_f64(const gb_testcase *tcs, int n, double *raw_d) {
-  GB_ARG(n >= 0 && raw_d, "gb_phmm_compute_f64: bad arguments");
+  GB_ARG(n >= 0 && raw_d && (n == 0 || tcs), "gb_phmm_compute_f64: bad arguments");
   if (n == 0) return GB_OK;
-  gb_phmm_batch *b = nullptr;
-  int st = gb_phmm_batch_create(tcs, n, &b);
+  DeviceTables *tabs = nullptr;
+  int st = get_device_tables(&tabs);
   if (st) return st;
+  gb_phmm_batch *b = thread_workspace(tabs, &st);
+  if (!b) return st;
+  if ((st = batch_fill(b, tcs, n))) return st;
   b->force_f64 = true;
   st = gb_phmm_batch_run(b);
+  b->force_f64 = false;
   if (!st) st = gb_phmm_batch_results(b, nullptr, nullptr, raw_d, nullptr, nullptr);
-  gb_phmm_batch_destroy(b);
   return st;
 }
 

@@ -68,10 +68,16 @@ int gb_bsw_batch_results(gb_bsw_batch *b, gb_seqpair *pairs, int32_t *out6, int3
 int gb_bsw_batch_timing(gb_bsw_batch *b, float *kernel_ms);
 int gb_bsw_batch_destroy(gb_bsw_batch *b);
 
-/* One-shot getScores16: results written into pairs in place. */
+/* One-shot getScores16: results written into pairs in place. Reuses one cached device batch per
+ * (calling thread, device), so calling it once per batch of pairs (main_banded.cpp:896-909) does
+ * not create streams or buffers per call. */
 int gb_bsw_get_scores16(const gb_bsw_params *params, gb_seqpair *pairs, int64_t num_pairs,
                         const uint8_t *seq_buf_ref, int64_t ref_bytes, const uint8_t *seq_buf_qer,
                         int64_t qer_bytes);
+/* The same, also returning the DP cells evaluated (SW_cells accounting of BandedPairWiseSW). */
+int gb_bsw_get_scores16_ex(const gb_bsw_params *params, gb_seqpair *pairs, int64_t num_pairs,
+                           const uint8_t *seq_buf_ref, int64_t ref_bytes, const uint8_t *seq_buf_qer,
+                           int64_t qer_bytes, int64_t *total_cells);
 
 #ifdef __cplusplus
 }
