@@ -5,17 +5,24 @@
 
 Metric (BASELINE.json): "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X".
 phmm (the line's `value`): a step = one PairHMM forward pass (f32 kernel + f64 fallback kernel +
-log10 epilogue) over one 'large'-shaped synthetic job of B batches (gen.phmm_dataset, seed 1 + rank)
-already resident in HBM; value = total cells of all ranks x K / max-over-ranks wall time, in GCUPS.
-chain / bsw (the "chain" / "bsw" objects): a step = chain_dp over every call of a 'large'-shaped
-set (10k calls, 25 M anchors, seed 5 + rank; Manchors/s) / the banded SW extension of every pair of
-a 'large'-shaped set (10 606 460 pairs, seed 11 + rank; GCUPS over the reference's inner-loop cells).
+log10 epilogue) over this rank's shard of one 'large'-shaped synthetic job of B batches
+(gen.phmm_dataset, seed 1) already resident in HBM; value = cells of the whole job x K / max-over-ranks
+wall time, in GCUPS.
+chain / bsw (the "chain" / "bsw" objects): a step = chain_dp over every call of the rank's shard of a
+'large'-shaped set (10k calls, 25 M anchors, seed 5; Manchors/s) / the banded SW extension of every
+pair of the rank's shard of a 'large'-shaped set (10 606 460 pairs, seed 11; GCUPS over the
+reference's inner-loop cells).
 fmi (the line's "fmi" object): a step = the whole fmi.cpp per-batch pipeline (SMEMs, reseeding,
-LAST seeds, per-read sort) over every read of the rank's shard (gen.fmi_reads, seed 8 + rank) against
-a 512 Mbp genome-like synthetic reference (+RC: 1.024 G BWT rows, 1.02 GB CP_OCC) built on the GPU;
-value = reads of all ranks x K / max-over-ranks wall time, in Mreads/s.
-Weak scaling: every rank processes its own shard of the same shape (independent shards, no
-data-path collective; torch.distributed only provides the barrier and the max-time reduction).
+LAST seeds, per-read sort) over every read of the rank's shard (whole 512-read batches) of a 10 M-read
+set (gen.fmi_reads, seed 8) against a 512 Mbp genome-like synthetic reference (+RC: 1.024 G BWT rows,
+1.02 GB CP_OCC) built on the GPU and replicated on every rank; value = reads x K / max-over-ranks time.
+"small" object: the same four legs on the 'small'-shaped sets (phmm small batches, 1 M fmi reads over
+the same index, 1 000 chain calls, 100 000 bsw pairs), sharded the same way.
+Strong scaling (default): every rank generates the same seeded set and keeps its contiguous shard
+(shard.py: testcases by cells, reads by whole batches, calls by anchors, pairs by cell estimate), so
+N GPUs share one fixed job and the shards concatenate back into the 1-GPU output. --scaling weak
+gives every rank its own full-size set (seed + rank) instead. There is no data-path collective;
+torch.distributed only provides the barrier and the max-time / sum-work reductions.
 """
 from __future__ import annotations
 
@@ -37,6 +44,7 @@ PEAK_F64_OPS = PEAK_F32_OPS / 2      # FP64 vector peak 78.6 TF (FMA=2) -> 39.3e
 PHMM_FLOP_PER_CELL = 12              # 12 FP ops per cell, no FMA
 PEAK_HBM = 8.0e12                    # HBM3E spec bytes/s (MI355X_MICROARCH.md)
 FMI_BYTES_PER_EXT = 128              # 2 x 64-B CP_OCC lines per backwardExt
+FMI_OCC_BYTES_PER_EXT = 35           # bytes of the one Occ32 line the kernel gathers per extension (DESIGN.md fmi)
 SA_BYTES_PER_STEP = 64               # one 64-B Occ2 line per LF step of an SA lookup
 SA_BYTES_PER_COORD = 24              # row in, sampled-SA entry, coordinate out (8 B each)
 CHAIN_OPS_PER_PAIR = 25              # ~25 int32/fp64 ops per visited (i, j) pair
@@ -175,25 +183,55 @@ def cpu_baseline_phmm(ta, sample_seconds: float):
                       f"job x {reps} passes, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
 
 
-def cpu_baseline_fmi(oracle_index, codes, lens, sample_seconds: float):
+def cpu_baseline_fmi(oracle_index, codes, lens, sample_seconds: float, fmi=None, idx=None):
     """The bwa-mem2 SMEM restatement (oracle/fmi_oracle.c, kind 'port': the reference FMI_search.cpp
-    is not buildable here without Palisade) over a bounded sample of the same reads."""
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    is not buildable here without Palisade) over a bounded sample (whole 512-read batches) of the same
+    reads. The sample's SMEM lists are compared with the GPU's on the same reads (bit-exact)."""
+    threads = max(1, min(16, _cores()))
     cal = min(len(lens), 4000 * threads)
     t0 = time.perf_counter()
     oracle_index.run_threaded(codes[:cal], lens[:cal], threads)
     rate = cal / max(time.perf_counter() - t0, 1e-6)
     m = int(min(len(lens), max(cal, rate * sample_seconds)))
+    m = min(len(lens), max(512, m // 512 * 512))
     t0 = time.perf_counter()
-    oracle_index.run_threaded(codes[:m], lens[:m], threads)
+    _, ocalls, parts = oracle_index.run_threaded(codes[:m], lens[:m], threads, collect=True)
     t = time.perf_counter() - t0
-    return {"value": m / t / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
+    check = None
+    if fmi is not None:
+        rs = fmi.Reads(idx, codes[:m], lens[:m])
+        rs.search(19)
+        sm, tot, bc, _ = rs.results(batch_size=512)
+        _, _, gcalls = rs.timing()
+        rs.close()
+        exp = np.concatenate(parts) if parts else sm[:0]
+        same = tot == len(exp) and all((sm[f] == exp[f]).all() for f in ("rid", "m", "n", "k", "l", "s"))
+        check = {"reads": m, "smems": int(tot), "bit_exact": bool(same), "backwardExt_equal": bool(gcalls == ocalls)}
+        if not (same and gcalls == ocalls):
+            raise SystemExit(f"fmi parity FAILED on the CPU-baseline sample: {check}")
+    port = {"value": m / t / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
             "sample": f"first {m} of {len(lens)} reads of the same shard, C restatement of bwa-mem2 "
-                      f"FMI_search (batches of 512 over {threads} threads), {t:.1f} s"}
+                      f"FMI_search (batches of 512 over {threads} threads), {t:.1f} s",
+            "parity_check": check}
+    # reference kind: bwa v1's own mem_collect_intv (tools/bwa, unmodified, oracle/_ref) over a bwt_t
+    # rebuilt from the same CP_OCC tables -- same intervals (tests/test_fmi_oracle.py), bwa v1 speed
+    import fmi_util
+    lib = fmi_util.ref_bwa()
+    if lib is None:
+        return port
+    n_, _, s_ = idx.info() if idx is not None else oracle_index.info()
+    bwt = fmi_util.bwa_from_tables(lib, n_, s_, oracle_index._occ)
+    t0 = time.perf_counter()
+    tot = fmi_util.bwa_collect_threaded(lib, bwt, codes[:m], lens[:m], threads)
+    t = time.perf_counter() - t0
+    lib.ref_bwa_free(bwt)
+    if check is not None and tot != check["smems"]:
+        raise SystemExit(f"bwa v1 interval count {tot} != GPU SMEM count {check['smems']} on the baseline sample")
+    return {"value": m / t / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "reference",
+            "sample": f"first {m} of {len(lens)} reads of the same shard, bwa v1 mem_collect_intv (tools/bwa "
+                      f"bwt_smem1 + bwt_seed_strategy1, compiled unmodified) over a bwt_t rebuilt from the same "
+                      f"CP_OCC tables, {threads} threads, {t:.1f} s; {tot} intervals == GPU SMEM count",
+            "port": port, "parity_check": check}
 
 
 def _cores():
@@ -283,48 +321,75 @@ def cpu_baseline_bsw(pairs, params, sample_seconds: float):
                       f"{threads} threads, {t:.1f} s"}
 
 
-def bench_chain(args, D, rank, world):
-    from genomicsbench_palisade_amd import chain, gen
-    log("chain: generating calls")
-    calls = gen.chain_dataset("large", seed=5 + rank)
+def set_seed(args, base: int, rank: int) -> int:
+    """Strong scaling: one set for the whole job (every rank the same seed, then its shard); weak:
+    every rank its own full-size set."""
+    return base if args.scaling == "strong" else base + rank
+
+
+def timed_steps(D, steps: int, step):
+    """Barrier + device sync on both sides of exactly `steps` calls of step() (each returns its kernel
+    ms); returns (max-over-ranks wall seconds, mean kernel ms of this rank)."""
+    D.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    ks = [step() for _ in range(steps)]
+    device_sync()
+    D.barrier()
+    return D.max(time.perf_counter() - t0), float(np.mean(ks)) if ks else 0.0
+
+
+def shard_note(args, what: str, lo: int, hi: int, total: int, world: int) -> str:
+    if args.scaling == "strong":
+        return f"{what} {lo}..{hi} of {total} (rank 0 shard of {world})" if world > 1 else f"all {total} {what}"
+    return f"{total} {what} per rank (own seed)"
+
+
+def bench_chain(args, D, rank, world, kind="large"):
+    from genomicsbench_palisade_amd import chain, gen, shard
+    log(f"chain {kind}: generating calls")
+    full = gen.chain_dataset(kind, seed=set_seed(args, 5, rank))
+    if args.scaling == "strong":
+        calls, (lo, hi) = shard.shard_calls(full, rank, world)
+    else:
+        calls, (lo, hi) = full, (0, full.ncalls)
     b = chain.ChainBatch(calls)
     for _ in range(args.warmup):
         b.run()
         b.sync()
     visited = b.results()[4]
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    ks = []
-    for _ in range(args.steps):
+
+    def step():
         b.run()
         b.sync()
-        ks.append(b.timing())
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
-    manch = D.sum(float(calls.nanchors)) * args.steps / elapsed / 1e6
-    ms = float(np.mean(ks))
+        return b.timing()
+    elapsed, ms = timed_steps(D, args.steps, step)
+    anchors_all = D.sum(float(calls.nanchors))
+    visited_all = D.sum(float(visited))
+    manch = anchors_all * args.steps / elapsed / 1e6
     ach = CHAIN_OPS_PER_PAIR * visited / (ms * 1e-3)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("chain: CPU baseline")
-        cpu = cpu_baseline_chain(calls, args.cpu_seconds)
-    bt = bench_chain_backtrack(args, D, rank, world, b, calls)
-    b.close()
-    return {
-        "backtrack": bt,
+    out = {
         "value": round(manch, 3), "unit": "Manchors/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "config": {"workload": f"chain large: {calls.ncalls} calls, {calls.nanchors} anchors/rank (lognormal "
-                               f"n, median 1500, max 87271), max_dist 5000, bw 500, n_segs 1",
-                   "visited_pairs": int(visited), "gpairs_per_s": visited * args.steps * D.world / elapsed / 1e9},
+        "config": {"workload": f"chain {kind}: {full.ncalls} calls, {full.nanchors} anchors in the set (lognormal n, "
+                               f"median 1500, max 87271), max_dist 5000, bw 500, n_segs 1; "
+                               + shard_note(args, "calls", lo, hi, full.ncalls, world),
+                   "anchors_all_ranks": int(anchors_all), "visited_pairs_all_ranks": int(visited_all),
+                   "gpairs_per_s": visited_all * args.steps / elapsed / 1e9},
         "roofline": {"bound": "valu", "kernel": "chain_kernel", "achieved": ach / 1e12, "peak": PEAK_CHAIN_OPS / 1e12,
-                     "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "traffic": pmc_traffic("chain_kernel"),
-                     "traffic_detail": pmc_traffic_detail("chain_kernel"),
-                     "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
+                     "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_kernel": ms},
-        "cpu_baseline": cpu,
     }
+    if kind == "large":
+        out["roofline"]["traffic"] = pmc_traffic("chain_kernel")
+        out["roofline"]["traffic_detail"] = pmc_traffic_detail("chain_kernel")
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            log("chain: CPU baseline")
+            cpu = cpu_baseline_chain(calls, args.cpu_seconds)
+        out["cpu_baseline"] = cpu
+        out["backtrack"] = bench_chain_backtrack(args, D, rank, world, b, calls)
+    b.close()
+    return out
 
 
 CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC = 3, 40  # minimap2 defaults (-n 3, -m 40)
@@ -339,19 +404,13 @@ def bench_chain_backtrack(args, D, rank, world, b, calls):
     b.backtrack(CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC)
     b.sync()
     nch, _, nan, _, _, tc, ta = b.chains()
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    ks = []
-    for _ in range(args.steps):
+
+    def step():
         b.backtrack(CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC)
         b.sync()
-        ks.append(b.backtrack_timing())
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
+        return b.backtrack_timing()
+    elapsed, ms = timed_steps(D, args.steps, step)
     manch = D.sum(float(calls.nanchors)) * args.steps / elapsed / 1e6
-    ms = float(np.mean(ks))
     ach = CHAIN_BT_BYTES_PER_ANCHOR * calls.nanchors / (ms * 1e-3)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -385,59 +444,68 @@ def bench_chain_backtrack(args, D, rank, world, b, calls):
     }
 
 
-def bench_bsw(args, D, rank, world):
-    from genomicsbench_palisade_amd import bsw, gen
-    log("bsw: generating pairs")
-    pairs = gen.bsw_dataset(args.bsw_pairs, seed=11 + rank, threads=min(16, _cores()))
+def bench_bsw(args, D, rank, world, kind="large"):
+    from genomicsbench_palisade_amd import bsw, gen, shard
+    log(f"bsw {kind}: generating pairs")
+    npairs = args.bsw_pairs if kind == "large" else gen.BSW_SMALL_PAIRS
+    full = gen.bsw_dataset(npairs, seed=set_seed(args, 11, rank), threads=min(16, _cores()))
+    if args.scaling == "strong":
+        pairs, (lo, hi) = shard.shard_pairs(full, rank, world)
+    else:
+        pairs, (lo, hi) = full, (0, full.n)
     params = bsw.default_params()
     b = bsw.BswBatch(pairs, params)
     for _ in range(args.warmup):
         b.run()
         b.sync()
     _, _, cells = b.results(want_cells=False)
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    ks = []
-    for _ in range(args.steps):
+
+    def step():
         b.run()
         b.sync()
-        ks.append(b.timing())
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
-    gcups = D.sum(float(cells)) * args.steps / elapsed / 1e9
-    ms = float(np.mean(ks))
+        return b.timing()
+    elapsed, ms = timed_steps(D, args.steps, step)
+    cells_all = D.sum(float(cells))
+    pairs_all = D.sum(float(pairs.n))
+    gcups = cells_all * args.steps / elapsed / 1e9
     ach = BSW_OPS_PER_CELL * cells / (ms * 1e-3)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("bsw: CPU baseline")
-        cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds)
-    b.close()
-    return {
+    out = {
         "value": round(gcups, 3), "unit": "GCUPS", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "config": {"workload": f"bsw large: {pairs.n} pairs/rank, query U[10,150], target = mutated query + "
-                               f"U[0,100], h0 0 (20%) or U[10,70], w 100, zdrop 100",
-                   "cells": int(cells), "mpairs_per_s": pairs.n * D.world * args.steps / elapsed / 1e6},
+        "config": {"workload": f"bsw {kind}: {full.n} pairs in the set, query U[10,150], target = mutated query + "
+                               f"U[0,100], h0 0 (20%) or U[10,70], w 100, zdrop 100; "
+                               + shard_note(args, "pairs", lo, hi, full.n, world),
+                   "cells_all_ranks": int(cells_all), "mpairs_per_s": pairs_all * args.steps / elapsed / 1e6},
         "roofline": {"bound": "valu", "kernel": "bsw_lane_kernel<NCH> (+ bsw_extend_kernel for long queries)",
-                     "achieved": ach / 1e12,
-                     "peak": PEAK_INT_OPS / 1e12, "unit": "T int op/s", "frac": ach / PEAK_INT_OPS,
-                     "traffic": pmc_traffic("bsw_lane_kernel"),
-                     "traffic_detail": pmc_traffic_detail("bsw_lane_kernel"), "ops_per_cell": BSW_OPS_PER_CELL},
+                     "achieved": ach / 1e12, "peak": PEAK_INT_OPS / 1e12, "unit": "T int op/s",
+                     "frac": ach / PEAK_INT_OPS, "ops_per_cell": BSW_OPS_PER_CELL},
         "kernels_ms": {"bsw (all launches of a step)": ms},
-        "cpu_baseline": cpu,
     }
+    if kind == "large":
+        out["roofline"]["traffic"] = pmc_traffic("bsw_lane_kernel")
+        out["roofline"]["traffic_detail"] = pmc_traffic_detail("bsw_lane_kernel")
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            log("bsw: CPU baseline")
+            cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds)
+        out["cpu_baseline"] = cpu
+    b.close()
+    return out
 
 
-def bench_phmm(args, D, rank, world):
+def bench_phmm(args, D, rank, world, kind="large"):
     import genomicsbench_palisade_amd as gb  # noqa: F401
-    from genomicsbench_palisade_amd import gen, phmm
+    from genomicsbench_palisade_amd import gen, phmm, shard
     from genomicsbench_palisade_amd._tc import TestcaseArray
 
     phmm.init_pairhmm()
-    log("phmm: generating + packing the job")
-    batches = gen.phmm_dataset("large", args.batches, seed=1 + rank)
-    ta = TestcaseArray.from_batches(batches)
+    nb = args.batches if kind == "large" else args.small_batches
+    log(f"phmm {kind}: generating + packing the job")
+    batches = gen.phmm_dataset(kind, nb, seed=set_seed(args, 1, rank))
+    full = TestcaseArray.from_batches(batches)
+    if args.scaling == "strong":
+        ta, (lo, hi) = shard.shard_testcases(full, rank, world)
+    else:
+        ta, (lo, hi) = full, (0, full.n)
     job = phmm.DeviceBatch(ta)
     ntc, cells, _ = job.stats()
     for _ in range(args.warmup):
@@ -448,43 +516,48 @@ def bench_phmm(args, D, rank, world):
     hl = ta.np_arr["haplen"][:ta.n].astype(np.int64)
     cells_f64 = int((rl * hl)[used.astype(bool)].sum())
 
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    k32, k64 = [], []
-    for _ in range(args.steps):
+    k64 = []
+
+    def step():
         job.run()
         job.sync()
         a, b, _ = job.timing()
-        k32.append(a)
         k64.append(b)
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
-    total_cells = D.sum(float(cells)) * args.steps
-    gcups = total_cells / elapsed / 1e9
-    ms32, ms64 = float(np.mean(k32)), float(np.mean(k64))
-    if ms32 >= ms64:
-        kern, ach, peak = "phmm_forward<float>", PHMM_FLOP_PER_CELL * cells / (ms32 * 1e-3), PEAK_F32_OPS
-    else:
-        kern, ach, peak = "phmm_forward<double>", PHMM_FLOP_PER_CELL * cells_f64 / (ms64 * 1e-3), PEAK_F64_OPS
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("phmm: CPU baseline")
-        cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
-    job.close()
-    return {
-        "value": gcups, "elapsed": elapsed, "ntc": ntc, "cells": cells, "f64_frac": float(used.mean()),
-        "roofline": {"bound": "valu", "kernel": kern, "achieved": ach / 1e12, "peak": peak / 1e12,
-                     "unit": "TFLOP/s (non-FMA FP ops)", "frac": ach / peak, "traffic": pmc_traffic(kern),
-                     "traffic_detail": pmc_traffic_detail(kern)},
+        return a
+    elapsed, ms32 = timed_steps(D, args.steps, step)
+    ms64 = float(np.mean(k64)) if k64 else 0.0
+    cells_all = D.sum(float(cells))
+    gcups = cells_all * args.steps / elapsed / 1e9
+    r32 = {"bound": "valu", "kernel": "phmm_forward<float>",
+           "achieved": PHMM_FLOP_PER_CELL * cells / (ms32 * 1e-3) / 1e12, "peak": PEAK_F32_OPS / 1e12,
+           "unit": "TFLOP/s (non-FMA FP ops)"}
+    r32["frac"] = r32["achieved"] / r32["peak"]
+    r64 = {"bound": "valu", "kernel": "phmm_forward<double> (f64 fallback, its testcases only)",
+           "achieved": PHMM_FLOP_PER_CELL * cells_f64 / max(ms64 * 1e-3, 1e-12) / 1e12, "peak": PEAK_F64_OPS / 1e12,
+           "unit": "TFLOP/s (non-FMA FP64 ops)", "cells": cells_f64}
+    r64["frac"] = r64["achieved"] / r64["peak"]
+    out = {
+        "value": gcups, "unit": "GCUPS", "elapsed": elapsed, "ntc": full.n, "cells": full.cells(), "cells_all_ranks": cells_all,
+        "f64_frac": float(used.mean()) if ta.n else 0.0,
+        "shard": shard_note(args, "testcases", lo, hi, full.n, world),
+        "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
-        "cpu_baseline": cpu,
     }
+    if kind == "large":
+        r32["traffic"] = pmc_traffic("phmm_forward<float>")
+        r32["traffic_detail"] = pmc_traffic_detail("phmm_forward<float>")
+        r64["traffic"] = pmc_traffic("phmm_forward<double>")
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            log("phmm: CPU baseline")
+            cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
+        out["cpu_baseline"] = cpu
+    job.close()
+    return out
 
 
 def bench_fmi(args, D, rank, world):
-    from genomicsbench_palisade_amd import fmi, gen
+    from genomicsbench_palisade_amd import fmi, gen, shard
 
     t0 = time.perf_counter()
     log("fmi: reference + GPU index build")
@@ -492,57 +565,97 @@ def bench_fmi(args, D, rank, world):
     idx = fmi.Index.build(ref)
     t_index = time.perf_counter() - t0
     log("fmi: generating reads")
-    codes, lens = gen.fmi_reads(ref, args.fmi_reads, read_len=151, seed=8 + rank)
+    codes_all, lens_all = gen.fmi_reads(ref, args.fmi_reads, read_len=151, seed=set_seed(args, 8, rank))
+    if args.scaling == "strong":
+        lo, hi = shard.read_range(len(lens_all), rank, world)
+    else:
+        lo, hi = 0, len(lens_all)
+    codes, lens = codes_all[lo:hi], lens_all[lo:hi]
     log("fmi: timed search")
     rs = fmi.Reads(idx, codes, lens)
     for _ in range(args.warmup):
         rs.search(19)
         rs.sync()
     _, total, _, phases = rs.results(batch_size=512, want_smems=False)
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    ks, kt, calls = [], [], 0
-    for _ in range(args.steps):
+    calls = [0]
+
+    def step():
         rs.search(19)
         rs.sync()
-        a, b, calls = rs.timing()
-        ks.append(a)
-        kt.append(b)
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
-    mreads = D.sum(float(len(lens))) * args.steps / elapsed / 1e6
-    ms = float(np.mean(ks))
+        a, _, calls[0] = rs.timing()
+        return a
+    elapsed, ms = timed_steps(D, args.steps, step)
+    calls = calls[0]
+    reads_all = D.sum(float(len(lens)))
+    mreads = reads_all * args.steps / elapsed / 1e6
     alg_bytes = calls * FMI_BYTES_PER_EXT + len(lens) * 151 + total * 40
+    occ_bytes = calls * FMI_OCC_BYTES_PER_EXT + len(lens) * 151 + total * 40
     ach = alg_bytes / (ms * 1e-3)
     cpu = None
+    n, _, _ = idx.info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import fmi_util
         n_, c_, s_ = idx.info()
         oi = fmi_util.OracleIndex(adopt=(n_, c_, s_, idx.cp_occ()))  # same tables, no CPU SA build
         log("fmi: CPU baseline")
-        cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds)
+        cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds, fmi, idx)
         oi.close()
-    n, _, _ = idx.info()
     sa = bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens)
     rs.close()
+    small = bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref)
     idx.close()
     return {
         "value": round(mreads, 3), "unit": "Mreads/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "config": {"workload": f"fmi large: {args.fmi_ref_mbp:g} Mbp synthetic genome-like reference "
-                               f"(BWT rows {n}), {len(lens)} reads x 151 bp/rank, minSeedLen 19, batch 512",
-                   "smems_per_read": total / len(lens), "num_smem1_2_3": [int(x) for x in phases],
-                   "backwardExt_per_read": calls / len(lens), "index_build_s": round(t_index, 2)},
+                               f"(BWT rows {n}), {len(lens_all)} reads x 151 bp in the set, minSeedLen 19, batch 512; "
+                               + shard_note(args, "reads", lo, hi, len(lens_all), world),
+                   "reads_all_ranks": int(reads_all),
+                   "smems_per_read": total / max(len(lens), 1), "num_smem1_2_3": [int(x) for x in phases],
+                   "backwardExt_per_read": calls / max(len(lens), 1), "index_build_s": round(t_index, 2)},
         "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9,
                      "unit": "GB/s", "frac": ach / PEAK_HBM, "traffic": pmc_traffic("smem_search"),
                      "traffic_detail": pmc_traffic_detail("smem_search"),
-                     "algorithmic_bytes": int(alg_bytes)},
-        "kernels_ms": {"smem_search": ms, "smem_search+scan": float(np.mean(kt))},
+                     "algorithmic_bytes": int(alg_bytes),
+                     "note": "achieved uses the reference's 128 B (two 64-B CP_OCC lines) per backwardExt; "
+                             "the kernel itself reads one Occ32 line (~35 B of it) per extension",
+                     "occ32_bytes": int(occ_bytes), "achieved_occ32": occ_bytes / (ms * 1e-3) / 1e9},
+        "kernels_ms": {"smem_search": ms},
         "cpu_baseline": cpu,
         "sa_lookup": sa,
+        "small": small,
     }
+
+
+def bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref):
+    """fmi 'small' (1 M reads, fmi_output:19) over the same index."""
+    log("fmi small: timed search")
+    codes_all, lens_all = gen.fmi_reads(ref, args.fmi_small_reads, read_len=151, seed=set_seed(args, 9, rank))
+    lo, hi = shard.read_range(len(lens_all), rank, world) if args.scaling == "strong" else (0, len(lens_all))
+    rs = fmi.Reads(idx, codes_all[lo:hi], lens_all[lo:hi])
+    for _ in range(args.warmup):
+        rs.search(19)
+        rs.sync()
+    calls = [0]
+
+    def step():
+        rs.search(19)
+        rs.sync()
+        a, _, calls[0] = rs.timing()
+        return a
+    elapsed, ms = timed_steps(D, args.steps, step)
+    _, total, _, _ = rs.results(batch_size=512, want_smems=False)
+    rs.close()
+    nr = hi - lo
+    alg = calls[0] * FMI_BYTES_PER_EXT + nr * 151 + total * 40
+    return {"value": round(D.sum(float(nr)) * args.steps / elapsed / 1e6, 3), "unit": "Mreads/s",
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "config": {"workload": f"fmi small: {len(lens_all)} reads x 151 bp over the large index; "
+                                   + shard_note(args, "reads", lo, hi, len(lens_all), world),
+                       "smems_per_read": total / max(nr, 1)},
+            "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": alg / (ms * 1e-3) / 1e9,
+                         "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": alg / (ms * 1e-3) / PEAK_HBM},
+            "kernels_ms": {"smem_search": ms}}
 
 
 def bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens):
@@ -552,21 +665,16 @@ def bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens):
     for _ in range(max(1, args.warmup)):
         rs.sa_run(fmi.MAX_OCC, fmi.SA_PREFETCH)
         rs.sync()
-    D.barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    kms = []
-    steps = ncoords = 0
-    for _ in range(args.steps):
+    st = [0, 0]
+
+    def step():
         rs.sa_run(fmi.MAX_OCC, fmi.SA_PREFETCH)
         rs.sync()
-        a, steps, ncoords = rs.sa_timing()
-        kms.append(a)
-    device_sync()
-    D.barrier()
-    elapsed = D.max(time.perf_counter() - t0)
+        a, st[0], st[1] = rs.sa_timing()
+        return a
+    elapsed, ms = timed_steps(D, args.steps, step)
+    steps, ncoords = st
     mcoords = D.sum(float(ncoords)) * args.steps / elapsed / 1e6
-    ms = float(np.mean(kms))
     # per coordinate: its row (8 B read), one sampled-SA entry (8 B), the coordinate (8 B written);
     # per LF step one 64-B Occ2 line
     alg_bytes = steps * SA_BYTES_PER_STEP + ncoords * SA_BYTES_PER_COORD
@@ -620,11 +728,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batches", type=int, default=16, help="'large' phmm batches per job (per rank)")
-    ap.add_argument("--fmi-reads", type=int, default=10_000_000, help="fmi reads per rank")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: one set sharded over the ranks (default); weak: a full set per rank")
+    ap.add_argument("--batches", type=int, default=64, help="'large' phmm batches in the job")
+    ap.add_argument("--small-batches", type=int, default=256, help="'small' phmm batches in the job")
+    ap.add_argument("--fmi-reads", type=int, default=10_000_000, help="fmi 'large' reads in the set")
+    ap.add_argument("--fmi-small-reads", type=int, default=1_000_000, help="fmi 'small' reads in the set")
     ap.add_argument("--fmi-ref-mbp", type=float, default=512.0)
-    ap.add_argument("--bsw-pairs", type=int, default=10_606_460, help="bsw pairs per rank (large set)")
+    ap.add_argument("--bsw-pairs", type=int, default=10_606_460, help="bsw pairs in the 'large' set")
     ap.add_argument("--only", default=None, help="comma list of legs: phmm,fmi,chain,bsw (default all)")
+    ap.add_argument("--no-small", action="store_true", help="skip the 'small'-set legs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -639,8 +752,22 @@ def main():
     fm = bench_fmi(args, D, rank, world) if "fmi" in legs else None
     ch = bench_chain(args, D, rank, world) if "chain" in legs else None
     bw = bench_bsw(args, D, rank, world) if "bsw" in legs else None
+    small = None
+    if not args.no_small:
+        small = {}
+        if "phmm" in legs:
+            small["phmm"] = bench_phmm(args, D, rank, world, kind="small")
+        if fm is not None:
+            small["fmi"] = fm.pop("small")
+        if "chain" in legs:
+            small["chain"] = bench_chain(args, D, rank, world, kind="small")
+        if "bsw" in legs:
+            small["bsw"] = bench_bsw(args, D, rank, world, kind="small")
+    elif fm is not None:
+        fm.pop("small", None)
 
     if rank == 0:
+        seeds = "seed" if args.scaling == "strong" else "seed + rank"
         line = {
             "metric": "GCUPS (phmm) + Mreads/s (fmi) on 'large' set at 1/2/4/8 MI355X",
             "value": round(ph["value"], 3) if ph else None,
@@ -650,23 +777,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ph["elapsed"] / args.steps * 1e3, 4) if ph else None,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32+f64 (phmm), int64 (fmi), int32/f64 (chain), int32 (bsw)",
-            "data": "synthetic ('large'-shaped PairHMM batches seed 1+rank; genome-like reference seed 7 "
-                    "+ 151 bp reads seed 8+rank for fmi; minimap2-shaped anchor calls seed 5+rank for chain; "
-                    "extension pairs seed 11+rank for bsw)",
-            "config": {"workload": ("phmm large: %d batches/rank, %d testcases, %.3f G cells/rank/step, "
-                                    "%.1f%% testcases on the f64 fallback" % (
-                                        args.batches, ph["ntc"], ph["cells"] / 1e9, 100 * ph["f64_frac"]))
+            "data": f"synthetic ('large'-shaped PairHMM batches {seeds} 1; genome-like reference seed 7 + 151 bp "
+                    f"reads {seeds} 8 for fmi; minimap2-shaped anchor calls {seeds} 5 for chain; extension pairs "
+                    f"{seeds} 11 for bsw)",
+            "config": {"workload": ("phmm large: %d batches, %d testcases, %.3f G cells per step (whole job); "
+                                    "%s; %.1f%% of rank 0's testcases on the f64 fallback" % (
+                                        args.batches, ph["ntc"], ph["cells"] / 1e9, ph["shard"], 100 * ph["f64_frac"]))
                        if ph else None,
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world} ({args.scaling} scaling, no data-path collective)"},
             "roofline": ph["roofline"] if ph else None,
+            "roofline_f64": ph["roofline_f64"] if ph else None,
             "kernels_ms": ph["kernels_ms"] if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
             "fmi": fm,
             "chain": ch,
             "bsw": bw,
+            "small": small,
         }
         print(json.dumps(line))
     D.close()

@@ -219,6 +219,12 @@ class ChainCalls:
     def nanchors(self):
         return int(self.offsets[-1])
 
+    def slice(self, lo: int, hi: int) -> "ChainCalls":
+        """Calls lo..hi-1 as their own CSR set (anchors copied, offsets rebased)."""
+        o0, o1 = int(self.offsets[lo]), int(self.offsets[hi])
+        return ChainCalls(self.offsets[lo:hi + 1] - o0, self.x[o0:o1].copy(), self.y[o0:o1].copy(),
+                          self.avg_qspan[lo:hi].copy(), self.params4[lo:hi].copy())
+
 
 def chain_call(rng, n: int):
     """One read's anchors: a collinear true locus (~85% of anchors, with small indel drift) plus
@@ -308,6 +314,16 @@ class BswPairs:
         qry = np.concatenate([self.qry[self.qoff[p]:self.qoff[p] + self.qlen[p]] for p in idx.tolist()]) \
             if len(idx) else np.zeros(0, np.uint8)
         return BswPairs(tgt, toff, tl.copy(), qry, qoff, ql.copy(), self.h0[idx].copy())
+
+    def slice(self, lo: int, hi: int) -> "BswPairs":
+        """Pairs lo..hi-1 (contiguous, so the sequence pools are sliced, not gathered)."""
+        if hi <= lo:
+            return self.subset(np.zeros(0, np.int64))
+        t0, t1 = int(self.toff[lo]), int(self.toff[hi - 1] + self.tlen[hi - 1])
+        q0, q1 = int(self.qoff[lo]), int(self.qoff[hi - 1] + self.qlen[hi - 1])
+        return BswPairs(self.tgt[t0:t1].copy(), (self.toff[lo:hi] - t0).astype(np.int64), self.tlen[lo:hi].copy(),
+                        self.qry[q0:q1].copy(), (self.qoff[lo:hi] - q0).astype(np.int64), self.qlen[lo:hi].copy(),
+                        self.h0[lo:hi].copy())
 
 
 def _ragged_local(lens):

@@ -111,3 +111,49 @@ void ref_bwa_ksw_batch(int64_t n, const uint8_t *tgt, const int64_t *toff, const
                        &o[1], &o[2], &o[3], &o[4], &o[5]);
   }
 }
+
+/* A bwa v1 bwt_t over the BWT of a bwa-mem2 .bwt.2bit.64 index (its CP_OCC one-hot words, rows 0..n-1,
+ * one row without a base = the sentinel): the $-removed BWT packed 16 bases per word the way
+ * bwt_B00 reads it, then bwa's own bwt_bwtupdate_core (tools/bwa/bwtindex.c:151) interleaves the
+ * occurrence counts and bwt_gen_cnt_table (bwt.c:42) fills the popcount table. Row numbering is
+ * unchanged (bwa v1's primary = the sentinel row), so intervals compare directly. */
+void *ref_bwa_from_cp_occ(const int64_t *cp_occ, int64_t n, int64_t sentinel) {
+  bwt_t *bwt = (bwt_t *)calloc(1, sizeof(bwt_t));
+  bwtint_t seq_len = (bwtint_t)(n - 1), c[4] = {0, 0, 0, 0};
+  bwt->primary = (bwtint_t)sentinel;
+  bwt->seq_len = seq_len;
+  bwt->bwt_size = (seq_len + 15) >> 4;
+  bwt->bwt = (uint32_t *)calloc(bwt->bwt_size, 4);
+  for (int64_t row = 0, k = 0; row < n; row++) {
+    if (row == sentinel) continue;
+    const int64_t *line = cp_occ + (row >> 6) * 8;
+    const uint64_t bit = 1ull << (63 - (row & 63));
+    uint32_t b = 0;
+    for (int x = 1; x < 4; x++)
+      if ((uint64_t)line[4 + x] & bit) b = (uint32_t)x;
+    c[b]++;
+    bwt->bwt[k >> 4] |= b << ((~k & 0xf) << 1);
+    k++;
+  }
+  bwt->L2[0] = 0;
+  for (int x = 0; x < 4; x++) bwt->L2[x + 1] = bwt->L2[x] + c[x];
+  bwt_bwtupdate_core(bwt);
+  bwt_gen_cnt_table(bwt);
+  return bwt;
+}
+
+/* mem_collect_intv (above) over reads [0, nreads) of a row-major code matrix; returns the total
+ * number of intervals (or -1 when a read overflows `cap`). One call per host thread. */
+int64_t ref_bwa_collect_batch(void *bwtp, const uint8_t *codes, const int32_t *lens, int64_t nreads,
+                              int64_t stride, int min_seed_len) {
+  const int64_t cap = 1 << 14;
+  int64_t *k = (int64_t *)malloc(cap * 8), *l = (int64_t *)malloc(cap * 8), *s = (int64_t *)malloc(cap * 8);
+  int32_t *m = (int32_t *)malloc(cap * 4), *nn = (int32_t *)malloc(cap * 4);
+  int64_t tot = 0;
+  for (int64_t r = 0; r < nreads && tot >= 0; r++) {
+    int64_t c = ref_bwa_collect(bwtp, codes + r * stride, lens[r], min_seed_len, k, l, s, m, nn, cap);
+    tot = c < 0 ? -1 : tot + c;
+  }
+  free(k); free(l); free(s); free(m); free(nn);
+  return tot;
+}

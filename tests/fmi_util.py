@@ -85,9 +85,10 @@ class OracleIndex:
         assert tot >= 0
         return out[:tot], bc, pc
 
-    def run_threaded(self, codes, lens, threads, batch_size=512, min_seed_len=19):
+    def run_threaded(self, codes, lens, threads, batch_size=512, min_seed_len=19, collect=False):
         """Batches split over `threads` OS threads (ctypes releases the GIL), each with its own
-        handle over the shared CP_OCC table; returns (total SMEMs, backwardExt calls)."""
+        handle over the shared CP_OCC table; returns (total SMEMs, backwardExt calls), plus with
+        collect=True the per-thread SMEM arrays in read order (rid rebased to the whole read set)."""
         from concurrent.futures import ThreadPoolExecutor
         codes = np.ascontiguousarray(codes, np.uint8)
         lens = np.ascontiguousarray(lens, np.int32)
@@ -106,10 +107,17 @@ class OracleIndex:
                                           maxlen, batch_size, min_seed_len, out.ctypes.data, cap, None, None)
             calls = self.lib.fmi_oracle_bwt_calls(h)
             self.lib.fmi_oracle_unshare(h)
+            if collect:
+                out = out[:tot].copy()
+                out["rid"] += lo
+                return tot, calls, out
             return tot, calls
 
         with ThreadPoolExecutor(threads) as ex:
             res = list(ex.map(work, range(threads)))
+        if collect:
+            return (sum(r[0] for r in res), sum(r[1] for r in res),
+                    [r[2] for r in res if len(r) == 3])
         return sum(r[0] for r in res), sum(r[1] for r in res)
 
     def bwt_calls(self):
@@ -181,7 +189,37 @@ def ref_bwa():
     lib.ref_bwa_collect.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, i64]
     lib.ref_bwa_collect.restype = i64
     lib.ref_bwa_sa.argtypes = [vp, ctypes.c_char_p, vp, i64, vp]
+    lib.ref_bwa_from_cp_occ.argtypes = [vp, i64, i64]
+    lib.ref_bwa_from_cp_occ.restype = vp
+    lib.ref_bwa_collect_batch.argtypes = [vp, vp, vp, i64, i64, ctypes.c_int]
+    lib.ref_bwa_collect_batch.restype = i64
     return lib
+
+
+def bwa_from_tables(lib, n, sentinel, cp_occ):
+    """bwa v1 bwt_t over the BWT held by bwa-mem2 CP_OCC tables (same row numbering)."""
+    cp = np.ascontiguousarray(cp_occ, np.int64)
+    return lib.ref_bwa_from_cp_occ(cp.ctypes.data, n, sentinel)
+
+
+def bwa_collect_threaded(lib, bwt, codes, lens, threads, min_seed_len=19):
+    """bwa v1 mem_collect_intv over every read, reads split over `threads` OS threads (ctypes
+    releases the GIL); returns the total interval count."""
+    from concurrent.futures import ThreadPoolExecutor
+    codes = np.ascontiguousarray(codes, np.uint8)
+    lens = np.ascontiguousarray(lens, np.int32)
+    parts = np.array_split(np.arange(len(lens)), threads)
+
+    def work(ix):
+        if len(ix) == 0:
+            return 0
+        lo, hi = int(ix[0]), int(ix[-1]) + 1
+        return lib.ref_bwa_collect_batch(bwt, codes[lo:hi].ctypes.data, lens[lo:hi].ctypes.data, hi - lo,
+                                         codes.shape[1], min_seed_len)
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(work, parts))
+    assert min(res) >= 0
+    return int(sum(res))
 
 
 def bwa_sa(lib, bwt, sa_path, rows):
@@ -214,3 +252,93 @@ def per_read(smems, nreads):
     for r, m, n, k, l, s in zip(smems["rid"], smems["m"], smems["n"], smems["k"], smems["l"], smems["s"]):
         out[int(r)].append((int(m), int(n), int(k), int(l), int(s)))
     return [sorted(x) for x in out]
+
+
+# ------------------------------------------------------------------ index structure (any size)
+def bwt_char(cp_occ, rows):
+    """BWT byte at each row from the CP_OCC one-hot words (bit 63 - (row & 63) of line row >> 6,
+    build_fm_index FMI_search.cpp:290-320); 4 where no base bit is set (the sentinel row)."""
+    rows = np.asarray(rows, np.int64)
+    line = cp_occ[rows >> 6]
+    bit = np.uint64(63) - (rows & 63).astype(np.uint64)
+    out = np.full(len(rows), 4, np.int64)
+    for b in range(4):
+        hit = ((line[:, 4 + b].view(np.uint64) >> bit) & np.uint64(1)).astype(bool)
+        out[hit] = b
+    return out
+
+
+def suffix_less(text, a, b, window=64):
+    """Vectorised lexicographic suffix comparison text[a:] < text[b:] with end-of-text smallest (the
+    order saisxx gives the reference's build, FMI_search.cpp:250). Returns a bool array."""
+    a = np.asarray(a, np.int64).copy()
+    b = np.asarray(b, np.int64).copy()
+    n = len(text)
+    res = np.zeros(len(a), bool)
+    todo = np.arange(len(a))
+    pad = np.concatenate([text.astype(np.int16), np.full(window, -1, np.int16)])
+    while len(todo):
+        ia, ib = a[todo], b[todo]
+        wa = pad[np.minimum(ia[:, None] + np.arange(window)[None, :], n + window - 1)]
+        wb = pad[np.minimum(ib[:, None] + np.arange(window)[None, :], n + window - 1)]
+        wa[ia[:, None] + np.arange(window)[None, :] >= n] = -1
+        wb[ib[:, None] + np.arange(window)[None, :] >= n] = -1
+        diff = wa != wb
+        anyd = diff.any(axis=1)
+        first = diff.argmax(axis=1)
+        r = np.arange(len(todo))
+        res[todo[anyd]] = wa[r[anyd], first[anyd]] < wb[r[anyd], first[anyd]]
+        # equal windows that ran into the end of text: the shorter suffix is smaller
+        ended = (~anyd) & ((ia + window >= n) | (ib + window >= n))
+        res[todo[ended]] = ia[ended] > ib[ended]
+        todo = todo[(~anyd) & ~ended]
+        a[todo] += window
+        b[todo] += window
+    return res
+
+
+def check_index_structure(ref, n, count5, sentinel, cp_occ, sa_sampled=None, sample=20000, seed=0):
+    """Size-independent invariants of a .bwt.2bit.64 index over text = ref + revcomp(ref) (+ '$'):
+    CP_OCC counts are the running popcounts of the one-hot words, every row holds exactly one base
+    except the sentinel, per-base totals equal the text's base counts, and -- on the sampled SA --
+    the sampled rows are distinct, in suffix order, and carry BWT[row] = text[SA[row] - 1]. Raises
+    AssertionError with the first violated invariant."""
+    text = np.concatenate([ref, (3 - ref[::-1]).astype(np.uint8)])
+    assert n == len(text) + 1
+    rows_total = (n >> 6) + 1
+    assert cp_occ.shape == (rows_total, 8)
+    oh = cp_occ[:, 4:].view(np.uint64)
+    cnt = cp_occ[:, :4]
+    pc = np.bitwise_count(oh).astype(np.int64)
+    assert (cnt[1:] == cnt[:-1] + pc[:-1]).all(), "cp_count is not the running popcount"
+    assert (cnt[0] == 0).all()
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert not (oh[:, i] & oh[:, j]).any(), "a BWT row carries two bases"
+    per_line = pc.sum(axis=1)
+    full = np.full(rows_total, 64, np.int64)
+    full[-1] = n - (rows_total - 1) * 64
+    full[sentinel >> 6] -= 1
+    assert (per_line == full).all(), "rows without a base other than the sentinel"
+    assert bwt_char(cp_occ, [sentinel])[0] == 4
+    c4 = np.bincount(text, minlength=4)[:4].astype(np.int64)
+    assert ((cnt[-1] + pc[-1]) == c4).all(), "per-base totals differ from the text"
+    exp5 = np.concatenate([[0], np.cumsum(c4)]) + 1
+    assert list(count5) == exp5.tolist(), (count5, exp5)
+    if sa_sampled is None:
+        return
+    ns = (n >> 3) + 1
+    sa = np.asarray(sa_sampled, np.int64)[:ns]
+    assert sa.min() >= 0 and sa.max() < n
+    seen = np.zeros(n, np.uint8)
+    seen[sa] = 1
+    assert int(seen.sum(dtype=np.int64)) == len(sa), "sampled SA entries repeat"
+    del seen
+    rng = np.random.default_rng(seed)
+    t = np.unique(rng.integers(0, ns, sample))
+    rows = t * 8
+    s = sa[t]
+    exp = np.where(s > 0, text[np.maximum(s - 1, 0)], 4)
+    assert (bwt_char(cp_occ, rows) == exp).all(), "BWT[row] != text[SA[row] - 1]"
+    t2 = t[t + 1 < ns]
+    assert suffix_less(text, sa[t2], sa[t2 + 1]).all(), "sampled SA rows out of suffix order"

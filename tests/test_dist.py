@@ -1,6 +1,9 @@
 """Multi-process (N>1) path on CPU: world_size-2 gloo process groups exercise bench.py's Dist
-(barrier, max-over-ranks time, sum-over-ranks work) and the shard -> compute -> concatenate flow
-of shard.py, with the C oracles standing in for the per-GPU kernels (CPU-only container)."""
+(barrier, max-over-ranks time, sum-over-ranks work), its timed_steps bracket and set_seed, and the
+strong-scaling shard -> compute -> concatenate flow bench.py uses for all four legs (shard.py:
+testcases by cells, whole 512-read batches, calls by anchors, pairs by cell estimate), with the C
+oracles standing in for the per-GPU kernels (CPU-only container): the two ranks' outputs
+concatenate to the 1-rank output exactly."""
 import json
 import os
 import socket
@@ -14,29 +17,44 @@ from conftest import ROOT
 from genomicsbench_palisade_amd import shard
 
 WORKER = r'''
-import json, os, sys
+import json, os, sys, types
 sys.path.insert(0, os.environ["GB_ROOT"]); sys.path.insert(0, os.path.join(os.environ["GB_ROOT"], "tests"))
 import numpy as np
-import bench, oracle_lib
+import bench, oracle_lib, fmi_util
 from genomicsbench_palisade_amd import gen, shard, bsw
+from genomicsbench_palisade_amd._tc import TestcaseArray
 world, rank, local = bench.dist_env()
 D = bench.Dist(world)
+args = types.SimpleNamespace(scaling="strong")
 D.barrier()
 mx = D.max(float(rank + 1))
 sm = D.sum(float(10 * (rank + 1)))
-# chain: shard calls by anchor count
-calls = gen.chain_dataset("small", num_calls=60, seed=3, median_n=200, max_n=3000)
-lo, hi = shard.rank_range(np.diff(calls.offsets), rank, world)
-o0, o1 = calls.offsets[lo], calls.offsets[hi]
-sub = gen.ChainCalls(calls.offsets[lo:hi + 1] - o0, calls.x[o0:o1], calls.y[o0:o1], calls.avg_qspan[lo:hi], calls.params4[lo:hi])
+el, ms = bench.timed_steps(D, 3, lambda: 1.5)
+# each leg exactly as bench.py takes it: the same seeded set on every rank, then this rank's shard
+calls = gen.chain_dataset("small", num_calls=60, seed=bench.set_seed(args, 3, rank), median_n=200, max_n=3000)
+sub, (lo, hi) = shard.shard_calls(calls, rank, world)
 sc = oracle_lib.chain_oracle(sub, 1)[0] if sub.ncalls else np.zeros(0, np.int32)
-# bsw: shard pairs by cell estimate
-pairs = gen.bsw_pairs(500, seed=4)
-blo, bhi = shard.rank_range(pairs.qlen.astype(np.int64) * pairs.tlen, rank, world)
-out = oracle_lib.bsw_oracle(pairs.subset(np.arange(blo, bhi)), bsw.default_params(), 1)[0]
+pairs = gen.bsw_pairs(500, seed=bench.set_seed(args, 4, rank))
+psub, _ = shard.shard_pairs(pairs, rank, world)
+out = oracle_lib.bsw_oracle(psub, bsw.default_params(), 1)[0]
+ta = TestcaseArray.from_batches(gen.phmm_dataset("small", 3, seed=bench.set_seed(args, 1, rank)))
+tsub, trange = shard.shard_testcases(ta, rank, world)
+pr = np.zeros(tsub.n); rf = np.zeros(tsub.n, np.float32); rd = np.zeros(tsub.n)
+import ctypes
+if tsub.n:
+    oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(tsub.arr), tsub.n, pr.ctypes.data, rf.ctypes.data, rd.ctypes.data, None, 1)
+ref = gen.fmi_reference(60_000, seed=5)
+codes, lens = gen.fmi_reads(ref, 1300, seed=bench.set_seed(args, 8, rank))
+rlo, rhi = shard.read_range(len(lens), rank, world)
+oi = fmi_util.OracleIndex(ref)
+fs, fbc, _ = oi.run(codes[rlo:rhi], lens[rlo:rhi], batch_size=512)
+fs["rid"] += rlo
 import torch.distributed as dist
 got = [None] * world
-dist.all_gather_object(got, {"chain": sc.tolist(), "bsw": out.tolist(), "max": mx, "sum": sm, "range": [lo, hi]})
+dist.all_gather_object(got, {"chain": sc.tolist(), "bsw": out.tolist(), "phmm": pr.tolist(), "trange": list(trange),
+                             "fmi": [list(map(int, t)) for t in zip(fs["rid"], fs["m"], fs["n"], fs["k"], fs["l"], fs["s"])],
+                             "fmi_bc": fbc.tolist(), "rrange": [rlo, rhi],
+                             "max": mx, "sum": sm, "range": [lo, hi], "timed_steps_ms": ms})
 if rank == 0:
     json.dump(got, open(os.environ["GB_OUT"], "w"))
 D.close()
@@ -94,3 +112,22 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
     pairs = gen.bsw_pairs(500, seed=4)
     fb = oracle_lib.bsw_oracle(pairs, bsw.default_params(), 1)[0]
     assert (np.array(got[0]["bsw"] + got[1]["bsw"], np.int32).reshape(-1, 6) == fb).all()
+    assert [g["timed_steps_ms"] for g in got] == [1.5, 1.5]
+    # phmm: testcase shards balanced by cells concatenate to the 1-rank results
+    import ctypes
+    from genomicsbench_palisade_amd._tc import TestcaseArray
+    ta = TestcaseArray.from_batches(gen.phmm_dataset("small", 3, seed=1))
+    pr, rf, rd = np.zeros(ta.n), np.zeros(ta.n, np.float32), np.zeros(ta.n)
+    oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(ta.arr), ta.n, pr.ctypes.data, rf.ctypes.data,
+                                          rd.ctypes.data, None, 1)
+    assert got[0]["trange"][1] == got[1]["trange"][0] and got[1]["trange"][1] == ta.n
+    assert (np.array(got[0]["phmm"] + got[1]["phmm"]).view(np.uint64) == pr.view(np.uint64)).all()
+    # fmi: whole 512-read batches per rank; SMEM lists and per-batch counts concatenate
+    import fmi_util
+    ref = gen.fmi_reference(60_000, seed=5)
+    codes, lens = gen.fmi_reads(ref, 1300, seed=8)
+    fs, fbc, _ = fmi_util.OracleIndex(ref).run(codes, lens, batch_size=512)
+    assert got[0]["rrange"] == [0, 1024] and got[1]["rrange"] == [1024, 1300]
+    exp = [list(map(int, t)) for t in zip(fs["rid"], fs["m"], fs["n"], fs["k"], fs["l"], fs["s"])]
+    assert got[0]["fmi"] + got[1]["fmi"] == exp
+    assert got[0]["fmi_bc"] + got[1]["fmi_bc"] == fbc.tolist()

@@ -1,0 +1,95 @@
+"""fmi at the bench's 'large' index size (512 Mbp reference + RC -> 1.024 G BWT rows, 1.02 GB CP_OCC):
+the GPU-built index satisfies every size-independent invariant of a .bwt.2bit.64 index (running
+popcount counts, one base per row, per-base totals, sampled SA distinct / suffix-ordered /
+BWT-consistent, LF walks landing on suffix-ordered rows), and the GPU SMEM search over it equals the
+oracle (oracle/fmi_oracle.c, the FMI_search.cpp:986-1326 restatement) on the same tables bit for
+bit: (rid, m, n, k, l, s) lists, per-batch counts, phase counts and backwardExt counts.
+
+The CPU half (test_index_checker_*) pins the checker itself against the oracle's own build."""
+import numpy as np
+import pytest
+
+import fmi_util
+from genomicsbench_palisade_amd import gen
+
+LARGE_MBP = 512
+
+
+def _file_tables(path):
+    raw = np.fromfile(path, np.uint8)
+    n = int(raw[:8].view(np.int64)[0])
+    sz = (n >> 6) + 1
+    o = 48
+    cp = raw[o:o + sz * 64].view(np.int64).reshape(sz, 8)
+    o += sz * 64
+    ns = (n >> 3) + 1
+    ms = raw[o:o + ns].view(np.int8).astype(np.int64)
+    ls = raw[o + ns:o + 5 * ns].view(np.uint32).astype(np.int64)
+    return n, cp, (ms << 32) | ls
+
+
+def test_index_checker_accepts_oracle_build_and_rejects_corruption(tmp_path):
+    ref = gen.fmi_reference(150_000, seed=12, repeat_frac=0.2)
+    p = str(tmp_path / "o.bwt.2bit.64")
+    oi = fmi_util.OracleIndex(ref, path_out=p)
+    n, c5, s = oi.info()
+    n2, cp, sa = _file_tables(p)
+    assert n2 == n
+    fmi_util.check_index_structure(ref, n, c5, s, cp, sa, sample=4000)
+    bad = sa.copy()
+    bad[[100, 101]] = bad[[101, 100]]
+    with pytest.raises(AssertionError):
+        fmi_util.check_index_structure(ref, n, c5, s, cp, bad, sample=len(sa) * 4)
+    bad_cp = cp.copy()
+    bad_cp[7, 5] ^= 1 << 9
+    with pytest.raises(AssertionError):
+        fmi_util.check_index_structure(ref, n, c5, s, bad_cp)
+    oi.close()
+
+
+def test_suffix_less_matches_python_sort():
+    rng = np.random.default_rng(3)
+    text = rng.integers(0, 2, 3000).astype(np.uint8)  # binary text: long common prefixes
+    a, b = rng.integers(0, 3000, 500), rng.integers(0, 3000, 500)
+    got = fmi_util.suffix_less(text, a, b, window=8)
+    t = text.tobytes()
+    exp = np.array([t[i:] < t[j:] for i, j in zip(a, b)])
+    assert (got == exp).all()
+
+
+@pytest.mark.gpu
+def test_large_index_and_search_vs_oracle():
+    from genomicsbench_palisade_amd import fmi, set_device
+    set_device(0)
+    ref = gen.fmi_reference(LARGE_MBP * 1_000_000, seed=7)  # the bench's reference (bench.py)
+    idx = fmi.Index.build(ref)
+    n, c5, sent = idx.info()
+    assert n == 2 * len(ref) + 1
+    cp = idx.cp_occ()
+    sa = idx.sampled_sa()
+    fmi_util.check_index_structure(ref, n, c5, sent, cp, sa, sample=20000, seed=1)
+    # LF walks from random rows (GPU): consecutive rows are in suffix order and carry BWT = text[SA-1]
+    rng = np.random.default_rng(2)
+    rows = np.unique(rng.integers(0, n - 1, 4000))
+    got = idx.sa_lookup(np.concatenate([rows, rows + 1]))
+    s0, s1 = got[:len(rows)], got[len(rows):]
+    text = np.concatenate([ref, (3 - ref[::-1]).astype(np.uint8)])
+    assert fmi_util.suffix_less(text, s0, s1).all()
+    assert (fmi_util.bwt_char(cp, rows) == np.where(s0 > 0, text[np.maximum(s0 - 1, 0)], 4)).all()
+    del text, sa
+    # SMEM search of a read sample over the 1.024 G-row index == the oracle on the same tables
+    codes, lens = gen.fmi_reads(ref, 20_000, read_len=151, seed=8)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(19)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    _, _, calls = rs.timing()
+    oi = fmi_util.OracleIndex(adopt=(n, c5, sent, cp))
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512)
+    assert tot == len(exp) and tot > 0
+    assert (bc == ebc).all() and (pc == epc).all()
+    for f in ("rid", "m", "n", "k", "l", "s"):
+        assert (sm[f] == exp[f]).all(), f
+    assert calls == oi.bwt_calls()
+    oi.close()
+    rs.close()
+    idx.close()
