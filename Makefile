@@ -18,8 +18,8 @@ HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(LIB)/obj/%.o,$(HIP_SRCS)) $(LIB)/obj/gb_c
 HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
 .PHONY: all ref clean oracle
-DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so
-all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle
+DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so $(LIB)/libgb_fmi_dropin.so
+all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle tests/_build/fmi_class_driver
 
 $(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIB)/obj
@@ -56,6 +56,11 @@ $(BIN)/fmi: $(PKG)/drivers/fmi_main.cpp $(LIB)/libgb.so
 $(BIN)/phmm: $(PKG)/drivers/phmm_main.cpp $(LIB)/libgb.so
 	@mkdir -p $(BIN)
 	$(HOSTCXX) $(HOSTFLAGS) -pthread -o $@ $< -L$(LIB) -lgb -Wl,-rpath,'$$ORIGIN/../lib'
+
+# test driver: benchmarks/fmi/fmi.cpp's batch loop over the FMI_search class (tests/test_fmi_dropin.py)
+tests/_build/fmi_class_driver: tests/cpp/fmi_class_driver.cpp $(LIB)/libgb_fmi_dropin.so include/gb_compat/FMI_search.h
+	@mkdir -p tests/_build
+	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb_fmi_dropin -lgb -Wl,-rpath,'$$ORIGIN/../../$(LIB)'
 
 oracle:
 	$(MAKE) -s -C oracle all

@@ -70,50 +70,6 @@ struct PList {  // one lane's view of its wave-interleaved scratch
   __device__ __forceinline__ void put(int e, const Ent &v) const { base[(size_t)e * 64] = pack_ent(v); }
 };
 
-struct DevIndex {
-  const Occ32 *occ;
-  int64_t count[5];
-  int64_t sentinel;
-};
-
-// Occ(b, p) for b = A, C, G, T from one Occ32 block (GET_OCC, FMI_search.h:81-89, over the same
-// counts): T = p - A - C - G - [sentinel < p].
-__device__ __forceinline__ void occ4(const Occ32 &L, int64_t p, int64_t sentinel, int64_t o[4]) {
-  occ32_acg(L, p, o[0], o[1], o[2]);
-  o[3] = p - o[0] - o[1] - o[2] - (sentinel < p ? 1 : 0);
-}
-
-// count[a] by selects over kernel-argument scalars: an indexed read would become a global load
-// issued after the Occ gather (a second dependent memory round trip per backwardExt)
-__device__ __forceinline__ int64_t count_of(const DevIndex &F, int a) {
-  return a == 0 ? F.count[0] : a == 1 ? F.count[1] : a == 2 ? F.count[2] : a == 3 ? F.count[3] : F.count[4];
-}
-
-// backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). One 32-byte block covers
-// 64 rows; when sp and ep share a block the second load is skipped.
-__device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l, int64_t s, int a,
-                                        int64_t &ko, int64_t &lo, int64_t &so) {
-  const int64_t sp = k, ep = k + s;
-  const int64_t bs = sp >> 6, be = ep >> 6;
-  // the second line only when sp and ep fall in different lines (a duplicate request for the same
-  // line measured 10 % slower overall than the occasional wait for A)
-  const Occ32 A = F.occ[bs];
-  Occ32 B;
-  if (be != bs)
-    B = F.occ[be];
-  else
-    B = A;
-  int64_t os[4], oe[4];
-  occ4(A, sp, F.sentinel, os);
-  occ4(B, ep, F.sentinel, oe);
-  const int64_t off = (k <= F.sentinel && k + s > F.sentinel) ? 1 : 0;
-  const int64_t s3 = oe[3] - os[3], s2 = oe[2] - os[2], s1 = oe[1] - os[1], s0 = oe[0] - os[0];
-  const int64_t l3 = l + off, l2 = l3 + s3, l1 = l2 + s2, l0 = l1 + s1;
-  ko = a == 0 ? F.count[0] + os[0] : a == 1 ? F.count[1] + os[1] : a == 2 ? F.count[2] + os[2] : F.count[3] + os[3];
-  so = a == 0 ? s0 : a == 1 ? s1 : a == 2 ? s2 : s3;
-  lo = a == 0 ? l0 : a == 1 ? l1 : a == 2 ? l2 : l3;
-}
-
 // byte codes -> 4-bit codes, 8 per word (base b of word w at bits 4*(b))
 __global__ void pack_q4(const uint8_t *__restrict__ qdb, int32_t stride, int32_t nreads, int32_t q4_stride,
                         uint32_t *__restrict__ q4) {
@@ -897,6 +853,17 @@ int gb_fmi_index_load(const char *path, gb_fmi_index **out) {
   }
   *out = idx;
   return GB_OK;
+}
+
+int gb_fmi_index_prepare(gb_fmi_index *idx) {
+  GB_ARG(idx, "gb_fmi_index_prepare: null index");
+  if (idx->d_occ32) return GB_OK;
+  GB_HIP(hipSetDevice(idx->device));
+  hipStream_t s;
+  GB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int st = gbfmi::ensure_occ32(idx, s);
+  (void)hipStreamDestroy(s);
+  return st;
 }
 
 int gb_fmi_index_info(gb_fmi_index *idx, int64_t *n, int64_t *count5, int64_t *sentinel) {

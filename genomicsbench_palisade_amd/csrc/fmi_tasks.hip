@@ -1,0 +1,587 @@
+// fmi_tasks.hip -- MI355X (gfx950) per-call SMEM kernels behind the FMI_search method adapter
+// (include/gb_compat/FMI_search.h, csrc/fmi_dropin.cpp).
+//
+// The fused search (fmi.hip) runs the whole fmi.cpp batch pipeline for a device-resident read set.
+// The reference's class API instead hands over one phase at a time, with caller-chosen inputs:
+//   getSMEMsOnePosOneThread          FMI_search.cpp:986-1180   task = (rid, x, min_intv)
+//   getSMEMsAllPosOneThread          FMI_search.cpp:1182-1241  task = (rid, min_intv), every x start
+//   bwtSeedStrategyAllPosOneThread   FMI_search.cpp:1243-1326  task = (read i, max_intv)
+// and expects the matchArray in the reference's emission order. One task per lane: the lane runs the
+// reference loop for its task (backwardExt over the same Occ32 blocks as the fused kernel, `prev` list
+// in a private global scratch row) and appends (SMEM, round) records to its slot; the host adapter
+// lays the slots out in reference order: OnePos and LAST in task order, AllPos round-major (each
+// round visits the still-active reads in rid_array order, FMI_search.cpp:1203-1236), which is a
+// stable merge of the per-task lists by round. Tasks whose output overflows the slot are re-run with
+// a slot sized to their count (the kernels are deterministic).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gb.h"
+#include "../../include/gb_fmi.h"
+#include "fmi_index.h"
+#include "gb_common.h"
+
+namespace gbfmi {
+namespace {
+
+enum TaskMode { kOnePos = 0, kAllPos = 1, kLast = 2 };
+
+struct TSmem {  // gb_smem with the round in the padding word
+  uint32_t rid, m, n, round;
+  int64_t k, l, s;
+};
+static_assert(sizeof(TSmem) == sizeof(gb_smem), "TSmem mirrors gb_smem");
+
+struct TEnt {  // one `prev` entry
+  int64_t k, l, s;
+  uint32_t m, n;
+};
+
+struct TaskArgs {
+  DevIndex F;
+  const uint8_t *qdb;
+  const int32_t *lens, *offs;  // per rid
+  const int32_t *rid;          // per task
+  const int16_t *qpos;         // per task (OnePos)
+  const int32_t *intv;         // per task: min_intv (OnePos / AllPos) or max_intv (LAST)
+  int32_t ntasks, min_seed_len, cap, maxlen;
+  TSmem *out;                  // task t: out[t * cap ...]
+  int32_t *counts;             // per task: records emitted (may exceed cap)
+  int16_t *next_pos;           // per task (OnePos)
+  int32_t *rounds;             // per task (AllPos)
+  TEnt *prev;                  // per task: maxlen + 1 entries
+  unsigned long long *calls;   // backwardExt calls (work counter)
+};
+
+__device__ __forceinline__ void emit(const TaskArgs &A, int t, int &cnt, uint32_t rid, const TEnt &e, uint32_t round) {
+  if (cnt < A.cap) {
+    TSmem o;
+    o.rid = rid;
+    o.m = e.m;
+    o.n = e.n;
+    o.round = round;
+    o.k = e.k;
+    o.l = e.l;
+    o.s = e.s;
+    A.out[(size_t)t * A.cap + cnt] = o;
+  }
+  cnt++;
+}
+
+// forward extension = backwardExt on the reverse-complement BWT with k/l swapped (FMI_search.cpp:1044-1056)
+__device__ __forceinline__ TEnt fwd_ext(const DevIndex &F, const TEnt &sm, int a, unsigned &calls) {
+  TEnt o = sm;
+  int64_t ko, lo, so;
+  bwt_ext(F, sm.l, sm.k, sm.s, 3 - a, ko, lo, so);
+  calls++;
+  o.k = lo;
+  o.l = ko;
+  o.s = so;
+  return o;
+}
+
+__device__ __forceinline__ TEnt bwd_ext(const DevIndex &F, const TEnt &sm, int a, unsigned &calls) {
+  TEnt o = sm;
+  bwt_ext(F, sm.k, sm.l, sm.s, a, o.k, o.l, o.s);
+  calls++;
+  return o;
+}
+
+// getSMEMsOnePosOneThread for one (rid, x) (FMI_search.cpp:1004-1178); returns next_x.
+__device__ int one_pos(const TaskArgs &A, int t, uint32_t rid, int x, int32_t min_intv, uint32_t round, int &cnt,
+                       unsigned &calls) {
+  const DevIndex &F = A.F;
+  const uint8_t *q = A.qdb + A.offs[rid];
+  const int len = A.lens[rid];
+  TEnt *prev = A.prev + (size_t)t * (A.maxlen + 1);
+  int next_x = x + 1;
+  int a = q[x];
+  if (a >= 4) return next_x;
+  TEnt sm;
+  sm.m = sm.n = (uint32_t)x;
+  sm.k = count_of(F, a);
+  sm.l = count_of(F, 3 - a);
+  sm.s = count_of(F, a + 1) - count_of(F, a);
+  int numPrev = 0;
+  for (int j = x + 1; j < len; j++) {
+    a = q[j];
+    next_x = j + 1;
+    if (a >= 4) break;
+    TEnt ns = fwd_ext(F, sm, a, calls);
+    ns.n = (uint32_t)j;
+    prev[numPrev] = sm;
+    numPrev += ns.s != sm.s ? 1 : 0;
+    if (ns.s < min_intv) {
+      next_x = j;
+      break;
+    }
+    sm = ns;
+  }
+  if (sm.s >= min_intv) prev[numPrev++] = sm;
+  for (int p = 0; p < numPrev / 2; p++) {
+    const TEnt tmp = prev[p];
+    prev[p] = prev[numPrev - p - 1];
+    prev[numPrev - p - 1] = tmp;
+  }
+  for (int j = x - 1; j >= 0; j--) {
+    int numCurr = 0;
+    int curr_s = -1;  // int in the reference: assigned from the int64 s (truncating)
+    a = q[j];
+    if (a > 3) break;
+    int p;
+    for (p = 0; p < numPrev; p++) {
+      const TEnt s0 = prev[p];
+      TEnt ns = bwd_ext(F, s0, a, calls);
+      ns.m = (uint32_t)j;
+      if (ns.s < min_intv && (s0.n - s0.m + 1) >= (uint32_t)A.min_seed_len) {
+        emit(A, t, cnt, rid, s0, round);
+        break;
+      }
+      if (ns.s >= min_intv && ns.s != (int64_t)curr_s) {
+        curr_s = (int)ns.s;
+        prev[numCurr++] = ns;
+        break;
+      }
+    }
+    p++;
+    for (; p < numPrev; p++) {
+      const TEnt s0 = prev[p];
+      TEnt ns = bwd_ext(F, s0, a, calls);
+      ns.m = (uint32_t)j;
+      if (ns.s >= min_intv && ns.s != (int64_t)curr_s) {
+        curr_s = (int)ns.s;
+        prev[numCurr++] = ns;
+      }
+    }
+    numPrev = numCurr;
+    if (numCurr == 0) break;
+  }
+  if (numPrev != 0 && (prev[0].n - prev[0].m + 1) >= (uint32_t)A.min_seed_len) emit(A, t, cnt, rid, prev[0], round);
+  return next_x;
+}
+
+// bwtSeedStrategyAllPosOneThread for read i (FMI_search.cpp:1256-1323)
+__device__ void last_seeds(const TaskArgs &A, int t, uint32_t i, int32_t max_intv, int &cnt, unsigned &calls) {
+  const DevIndex &F = A.F;
+  const uint8_t *q = A.qdb + A.offs[i];
+  const int len = A.lens[i];
+  int x = 0;
+  while (x < len) {
+    int next_x = x + 1;
+    int a = q[x];
+    if (a < 4) {
+      TEnt sm;
+      sm.m = sm.n = (uint32_t)x;
+      sm.k = count_of(F, a);
+      sm.l = count_of(F, 3 - a);
+      sm.s = count_of(F, a + 1) - count_of(F, a);
+      for (int j = x + 1; j < len; j++) {
+        next_x = j + 1;
+        a = q[j];
+        if (a >= 4) break;
+        TEnt ns = fwd_ext(F, sm, a, calls);
+        ns.n = (uint32_t)j;
+        sm = ns;
+        if (sm.s < max_intv && (sm.n - sm.m + 1) >= (uint32_t)A.min_seed_len) {
+          if (sm.s > 0) emit(A, t, cnt, i, sm, 0);
+          break;
+        }
+      }
+    }
+    x = (int16_t)next_x;
+  }
+}
+
+template <int kMode>
+__global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned calls = 0;
+  if (t < A.ntasks) {
+    const uint32_t rid = (uint32_t)A.rid[t];
+    int cnt = 0;
+    if (kMode == kOnePos) {
+      A.next_pos[t] = (int16_t)one_pos(A, t, rid, A.qpos[t], A.intv[t], 0, cnt, calls);
+    } else if (kMode == kAllPos) {
+      const int len = A.lens[rid];
+      int x = 0;
+      uint32_t round = 0;
+      while (x < len) {  // the do-while of FMI_search.cpp:1203-1236 as seen by this read
+        x = (int16_t)one_pos(A, t, rid, x, A.intv[t], round, cnt, calls);
+        round++;
+      }
+      A.rounds[t] = (int32_t)round;
+    } else {
+      last_seeds(A, t, rid, A.intv[t], cnt, calls);
+    }
+    A.counts[t] = cnt;
+  }
+  // one atomic per wave for the work counter
+  for (int off = 32; off > 0; off >>= 1) calls += __shfl_down(calls, off, 64);
+  if ((threadIdx.x & 63) == 0 && calls) atomicAdd(A.calls, (unsigned long long)calls);
+}
+
+// Per host thread and device: stream and grow-only device buffers (the reference's methods are
+// called from OpenMP threads sharing one FMI_search object).
+struct Workspace {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  void *buf[10] = {nullptr};
+  size_t cap[10] = {0};
+  ~Workspace() {
+    if (device < 0) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    for (void *p : buf) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
+    (void)hipSetDevice(cur);
+  }
+  hipError_t ensure(int slot, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (cap[slot] >= bytes) return hipSuccess;
+    (void)hipFree(buf[slot]);
+    buf[slot] = nullptr;
+    cap[slot] = 0;
+    hipError_t e = hipMalloc(&buf[slot], bytes + bytes / 2);
+    if (e == hipSuccess) cap[slot] = bytes + bytes / 2;
+    return e;
+  }
+};
+
+Workspace &workspace(int device) {
+  static thread_local std::vector<Workspace *> ws;
+  if ((int)ws.size() <= device) ws.resize(device + 1, nullptr);
+  if (!ws[device]) {
+    ws[device] = new Workspace();
+    ws[device]->device = device;
+  }
+  return *ws[device];
+}
+
+struct HostTasks {
+  std::vector<int32_t> rid, intv;
+  std::vector<int16_t> qpos;
+};
+
+// Runs `mode` over the given tasks; fills per-task record lists (reference emission order within a
+// task) and per-task next_pos / rounds. Overflowing tasks are re-run with a larger slot.
+int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *lens, const int32_t *offs, int32_t nrid,
+              const HostTasks &T, int32_t min_seed_len, std::vector<std::vector<TSmem>> &recs,
+              std::vector<int16_t> *next_pos, std::vector<int32_t> *rounds, int64_t *calls_out) {
+  const int32_t ntasks = (int32_t)T.rid.size();
+  recs.assign(ntasks, {});
+  if (next_pos) next_pos->assign(ntasks, 0);
+  if (rounds) rounds->assign(ntasks, 0);
+  if (calls_out) *calls_out = 0;
+  if (ntasks == 0) return GB_OK;
+  // extent of enc_qdb the tasks read, and the longest read (prev scratch rows)
+  int64_t extent = 0;
+  int32_t maxlen = 1;
+  for (int32_t t = 0; t < ntasks; t++) {
+    const int32_t r = T.rid[t];
+    GB_ARG(r >= 0 && r < nrid, "FMI_search: task %d names read %d outside [0, %d)", t, r, nrid);
+    GB_ARG(lens[r] >= 0 && lens[r] < 32768 && offs[r] >= 0, "FMI_search: read %d has length %d / offset %d", r,
+           lens[r], offs[r]);
+    if (mode == kOnePos)
+      GB_ARG(T.qpos[t] >= 0 && T.qpos[t] < lens[r], "FMI_search: query position %d outside read %d (length %d)",
+             T.qpos[t], r, lens[r]);
+    extent = std::max<int64_t>(extent, (int64_t)offs[r] + lens[r]);
+    maxlen = std::max(maxlen, lens[r]);
+  }
+  GB_HIP(hipSetDevice(idx->device));
+  Workspace &W = workspace(idx->device);
+  if (!W.stream) GB_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+  if (int st = ensure_occ32(idx, W.stream)) return st;
+
+  TaskArgs A;
+  A.F.occ = idx->d_occ32;
+  for (int b = 0; b < 5; b++) A.F.count[b] = idx->count[b];
+  A.F.sentinel = idx->sentinel;
+  A.min_seed_len = min_seed_len;
+  A.maxlen = maxlen;
+
+  // the whole task set, then the overflowing subset with a slot sized to its largest count
+  std::vector<int32_t> todo(ntasks);
+  for (int32_t t = 0; t < ntasks; t++) todo[t] = t;
+  int32_t cap = mode == kLast ? 48 : 32;
+  for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
+    const int32_t n = (int32_t)todo.size();
+    std::vector<int32_t> rid(n), intv(n);
+    std::vector<int16_t> qpos(n);
+    for (int32_t i = 0; i < n; i++) {
+      rid[i] = T.rid[todo[i]];
+      intv[i] = T.intv[todo[i]];
+      qpos[i] = mode == kOnePos ? T.qpos[todo[i]] : 0;
+    }
+    hipError_t e = W.ensure(0, (size_t)extent);
+    if (e == hipSuccess) e = W.ensure(1, sizeof(int32_t) * (size_t)nrid);
+    if (e == hipSuccess) e = W.ensure(2, sizeof(int32_t) * (size_t)nrid);
+    if (e == hipSuccess) e = W.ensure(3, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = W.ensure(4, sizeof(int16_t) * (size_t)n);
+    if (e == hipSuccess) e = W.ensure(5, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = W.ensure(6, sizeof(TSmem) * (size_t)n * cap);
+    if (e == hipSuccess) e = W.ensure(7, sizeof(int32_t) * 2 * (size_t)n + sizeof(int16_t) * (size_t)n + 64);
+    if (e == hipSuccess) e = W.ensure(8, sizeof(TEnt) * (size_t)n * (maxlen + 1));
+    if (e == hipSuccess) e = W.ensure(9, sizeof(unsigned long long));
+    GB_HIP(e);
+    A.qdb = (const uint8_t *)W.buf[0];
+    A.lens = (const int32_t *)W.buf[1];
+    A.offs = (const int32_t *)W.buf[2];
+    A.rid = (const int32_t *)W.buf[3];
+    A.qpos = (const int16_t *)W.buf[4];
+    A.intv = (const int32_t *)W.buf[5];
+    A.out = (TSmem *)W.buf[6];
+    A.counts = (int32_t *)W.buf[7];
+    A.rounds = A.counts + n;
+    A.next_pos = (int16_t *)(A.rounds + n);
+    A.prev = (TEnt *)W.buf[8];
+    A.calls = (unsigned long long *)W.buf[9];
+    A.ntasks = n;
+    A.cap = cap;
+    hipStream_t s = W.stream;
+    if (pass == 0) {
+      GB_HIP(hipMemcpyAsync(W.buf[0], qdb, (size_t)extent, hipMemcpyHostToDevice, s));
+      GB_HIP(hipMemcpyAsync(W.buf[1], lens, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
+      GB_HIP(hipMemcpyAsync(W.buf[2], offs, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
+      GB_HIP(hipMemsetAsync(W.buf[9], 0, sizeof(unsigned long long), s));
+    }
+    GB_HIP(hipMemcpyAsync(W.buf[3], rid.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    GB_HIP(hipMemcpyAsync(W.buf[4], qpos.data(), sizeof(int16_t) * n, hipMemcpyHostToDevice, s));
+    GB_HIP(hipMemcpyAsync(W.buf[5], intv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    const dim3 grid((unsigned)((n + 63) / 64)), block(64);
+    if (mode == kOnePos)
+      hipLaunchKernelGGL(fmi_task_kernel<kOnePos>, grid, block, 0, s, A);
+    else if (mode == kAllPos)
+      hipLaunchKernelGGL(fmi_task_kernel<kAllPos>, grid, block, 0, s, A);
+    else
+      hipLaunchKernelGGL(fmi_task_kernel<kLast>, grid, block, 0, s, A);
+    GB_HIP(hipGetLastError());
+    std::vector<int32_t> ctl(2 * (size_t)n);
+    std::vector<int16_t> np(n);
+    std::vector<TSmem> out((size_t)n * cap);
+    GB_HIP(hipMemcpyAsync(ctl.data(), A.counts, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, s));
+    GB_HIP(hipMemcpyAsync(np.data(), A.next_pos, sizeof(int16_t) * n, hipMemcpyDeviceToHost, s));
+    GB_HIP(hipMemcpyAsync(out.data(), A.out, sizeof(TSmem) * (size_t)n * cap, hipMemcpyDeviceToHost, s));
+    unsigned long long calls = 0;
+    if (pass == 0) GB_HIP(hipMemcpyAsync(&calls, A.calls, sizeof(calls), hipMemcpyDeviceToHost, s));
+    GB_HIP(hipStreamSynchronize(s));
+    if (pass == 0 && calls_out) *calls_out = (int64_t)calls;
+    std::vector<int32_t> again;
+    int32_t need = 0;
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t t = todo[i], c = ctl[i];
+      if (c > cap) {
+        again.push_back(t);
+        need = std::max(need, c);
+        continue;
+      }
+      recs[t].assign(out.begin() + (size_t)i * cap, out.begin() + (size_t)i * cap + c);
+      if (next_pos) (*next_pos)[t] = np[i];
+      if (rounds) (*rounds)[t] = ctl[n + i];
+    }
+    todo.swap(again);
+    cap = need;
+  }
+  GB_ARG(todo.empty(), "FMI_search: SMEM output of %zu tasks could not be sized", todo.size());
+  return GB_OK;
+}
+
+// raw sampled-SA entries (get_sa_entry / get_sa_entries, FMI_search.cpp:1566-1619: sa_ms_byte << 32
+// + sa_ls_word at the given index of the sampled arrays)
+__global__ void sa_raw_kernel(const int64_t *__restrict__ sa, const int64_t *__restrict__ pos, int64_t n,
+                              int64_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = sa[pos[i]];
+}
+
+// call_one_step (FMI_search.cpp:1834-1893) on the reference CP_OCC lines
+__global__ void sa_one_step_kernel(const CpOcc *__restrict__ occ, const int64_t *__restrict__ sa, DevIndex F,
+                                   int64_t pos, int64_t offset, int64_t *out3) {
+  int64_t ret, entry;
+  if ((pos & 7) == 0) {
+    entry = sa[pos >> 3];
+    ret = 1;
+  } else {
+    const CpOcc &L = occ[pos >> 6];
+    const int y = 63 - (int)(pos & 63);
+    int b = 4;
+    for (int c = 3; c >= 0; c--)
+      if ((L.one_hot_bwt_str[c] >> y) & 1) b = c;
+    if (b == 4) {
+      entry = 0;
+      ret = 1;
+    } else {
+      const uint64_t mask = (pos & 63) ? ~0ull << (64 - (pos & 63)) : 0ull;
+      const int64_t sp = count_of(F, b) + L.cp_count[b] + __popcll(L.one_hot_bwt_str[b] & mask);
+      offset++;
+      if ((sp & 7) == 0) {
+        entry = sa[sp >> 3] + offset;
+        ret = 1;
+      } else {
+        entry = sp;
+        ret = 0;
+      }
+    }
+  }
+  out3[0] = ret;
+  out3[1] = entry;
+  out3[2] = offset;
+}
+
+void put(gb_smem *dst, const TSmem &r) {
+  gb_smem o;
+  std::memset(&o, 0, sizeof(o));
+  o.rid = r.rid;
+  o.m = r.m;
+  o.n = r.n;
+  o.k = r.k;
+  o.l = r.l;
+  o.s = r.s;
+  *dst = o;
+}
+
+}  // namespace
+}  // namespace gbfmi
+
+using namespace gbfmi;
+
+extern "C" {
+
+int gb_fmi_smem_onepos(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                       int32_t nrid, const int16_t *query_pos, const int32_t *min_intv, const int32_t *rid,
+                       int32_t ntasks, int32_t min_seed_len, gb_smem *out, int64_t out_cap, int64_t *nout,
+                       int16_t *next_pos, int64_t *bwt_calls) {
+  GB_ARG(idx && nout && ntasks >= 0 && nrid >= 0, "gb_fmi_smem_onepos: bad arguments");
+  GB_ARG(ntasks == 0 || (enc_qdb && lens && offs && query_pos && min_intv && rid), "gb_fmi_smem_onepos: null array");
+  HostTasks T;
+  T.rid.assign(rid, rid + ntasks);
+  T.intv.assign(min_intv, min_intv + ntasks);
+  T.qpos.assign(query_pos, query_pos + ntasks);
+  std::vector<std::vector<TSmem>> recs;
+  std::vector<int16_t> np;
+  int st = run_tasks(idx, kOnePos, enc_qdb, lens, offs, nrid, T, min_seed_len, recs, &np, nullptr, bwt_calls);
+  if (st) return st;
+  int64_t tot = 0;
+  for (auto &v : recs) tot += (int64_t)v.size();
+  *nout = tot;
+  if (next_pos) std::copy(np.begin(), np.end(), next_pos);
+  if (!out) return GB_OK;
+  GB_ARG(tot <= out_cap, "gb_fmi_smem_onepos: %lld SMEMs exceed out_cap %lld", (long long)tot, (long long)out_cap);
+  int64_t o = 0;
+  for (auto &v : recs)
+    for (auto &r : v) put(out + o++, r);
+  return GB_OK;
+}
+
+int gb_fmi_smem_allpos(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                       int32_t nrid, const int32_t *min_intv, const int32_t *rid, int32_t ntasks,
+                       int32_t min_seed_len, gb_smem *out, int64_t out_cap, int64_t *nout, int32_t *rounds,
+                       int64_t *bwt_calls) {
+  GB_ARG(idx && nout && ntasks >= 0 && nrid >= 0, "gb_fmi_smem_allpos: bad arguments");
+  GB_ARG(ntasks == 0 || (enc_qdb && lens && offs && min_intv && rid), "gb_fmi_smem_allpos: null array");
+  HostTasks T;
+  T.rid.assign(rid, rid + ntasks);
+  T.intv.assign(min_intv, min_intv + ntasks);
+  std::vector<std::vector<TSmem>> recs;
+  std::vector<int32_t> rn;
+  int st = run_tasks(idx, kAllPos, enc_qdb, lens, offs, nrid, T, min_seed_len, recs, nullptr, &rn, bwt_calls);
+  if (st) return st;
+  int64_t tot = 0;
+  int32_t max_round = 0;
+  for (int32_t t = 0; t < ntasks; t++) {
+    tot += (int64_t)recs[t].size();
+    max_round = std::max(max_round, rn[t]);
+  }
+  *nout = tot;
+  if (rounds) std::copy(rn.begin(), rn.end(), rounds);
+  if (!out) return GB_OK;
+  GB_ARG(tot <= out_cap, "gb_fmi_smem_allpos: %lld SMEMs exceed out_cap %lld", (long long)tot, (long long)out_cap);
+  // round-major, tasks in order within a round: a merge of the per-task lists (rounds ascending)
+  std::vector<size_t> cur(ntasks, 0);
+  std::vector<int32_t> live;
+  for (int32_t t = 0; t < ntasks; t++)
+    if (!recs[t].empty()) live.push_back(t);
+  int64_t o = 0;
+  for (uint32_t r = 0; r < (uint32_t)max_round && !live.empty(); r++) {
+    size_t w = 0;
+    for (int32_t t : live) {
+      auto &v = recs[t];
+      size_t &c = cur[t];
+      while (c < v.size() && v[c].round == r) put(out + o++, v[c++]);
+      if (c < v.size()) live[w++] = t;
+    }
+    live.resize(w);
+  }
+  return o == tot ? GB_OK : (gb::set_error("gb_fmi_smem_allpos: round merge lost records"), GB_ERR_STATE);
+}
+
+int gb_fmi_last_seeds(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                      int32_t nreads, const int32_t *max_intv, int32_t min_seed_len, gb_smem *out, int64_t out_cap,
+                      int64_t *nout, int64_t *bwt_calls) {
+  GB_ARG(idx && nout && nreads >= 0, "gb_fmi_last_seeds: bad arguments");
+  GB_ARG(nreads == 0 || (enc_qdb && lens && offs && max_intv), "gb_fmi_last_seeds: null array");
+  HostTasks T;
+  T.rid.resize(nreads);
+  for (int32_t i = 0; i < nreads; i++) T.rid[i] = i;
+  T.intv.assign(max_intv, max_intv + nreads);
+  std::vector<std::vector<TSmem>> recs;
+  int st = run_tasks(idx, kLast, enc_qdb, lens, offs, nreads, T, min_seed_len, recs, nullptr, nullptr, bwt_calls);
+  if (st) return st;
+  int64_t tot = 0;
+  for (auto &v : recs) tot += (int64_t)v.size();
+  *nout = tot;
+  if (!out) return GB_OK;
+  GB_ARG(tot <= out_cap, "gb_fmi_last_seeds: %lld SMEMs exceed out_cap %lld", (long long)tot, (long long)out_cap);
+  int64_t o = 0;
+  for (auto &v : recs)
+    for (auto &r : v) put(out + o++, r);
+  return GB_OK;
+}
+
+int gb_fmi_sa_raw(gb_fmi_index *idx, const int64_t *pos, int64_t n, int64_t *out) {
+  GB_ARG(idx && n >= 0 && (n == 0 || (pos && out)), "gb_fmi_sa_raw: bad arguments");
+  for (int64_t i = 0; i < n; i++)
+    GB_ARG(pos[i] >= 0 && pos[i] < idx->sa_ns, "gb_fmi_sa_raw: index %lld outside the %lld sampled entries",
+           (long long)pos[i], (long long)idx->sa_ns);
+  if (n == 0) return GB_OK;
+  GB_HIP(hipSetDevice(idx->device));
+  Workspace &W = workspace(idx->device);
+  if (!W.stream) GB_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+  GB_HIP(W.ensure(3, sizeof(int64_t) * 2 * (size_t)n));
+  int64_t *d = (int64_t *)W.buf[3];
+  GB_HIP(hipMemcpyAsync(d, pos, sizeof(int64_t) * n, hipMemcpyHostToDevice, W.stream));
+  hipLaunchKernelGGL(sa_raw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, W.stream, idx->d_sa, d, n, d + n);
+  GB_HIP(hipGetLastError());
+  GB_HIP(hipMemcpyAsync(out, d + n, sizeof(int64_t) * n, hipMemcpyDeviceToHost, W.stream));
+  GB_HIP(hipStreamSynchronize(W.stream));
+  return GB_OK;
+}
+
+int gb_fmi_sa_one_step(gb_fmi_index *idx, int64_t pos, int64_t *sa_entry, int64_t *offset, int32_t *done) {
+  GB_ARG(idx && sa_entry && offset && done, "gb_fmi_sa_one_step: null argument");
+  GB_ARG(pos >= 0 && pos < idx->n, "gb_fmi_sa_one_step: row %lld outside [0, %lld)", (long long)pos, (long long)idx->n);
+  GB_HIP(hipSetDevice(idx->device));
+  Workspace &W = workspace(idx->device);
+  if (!W.stream) GB_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
+  GB_HIP(W.ensure(9, 4 * sizeof(int64_t)));
+  DevIndex F;
+  F.occ = nullptr;
+  for (int b = 0; b < 5; b++) F.count[b] = idx->count[b];
+  F.sentinel = idx->sentinel;
+  int64_t *d = (int64_t *)W.buf[9];
+  hipLaunchKernelGGL(sa_one_step_kernel, dim3(1), dim3(1), 0, W.stream, idx->d_occ, idx->d_sa, F, pos, *offset, d);
+  GB_HIP(hipGetLastError());
+  int64_t r[3];
+  GB_HIP(hipMemcpyAsync(r, d, sizeof(r), hipMemcpyDeviceToHost, W.stream));
+  GB_HIP(hipStreamSynchronize(W.stream));
+  *done = (int32_t)r[0];
+  *sa_entry = r[1];
+  *offset = r[2];
+  return GB_OK;
+}
+
+}  // extern "C"

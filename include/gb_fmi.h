@@ -42,6 +42,9 @@ int gb_fmi_index_load(const char *bwt_2bit_64_path, gb_fmi_index **out);
  * receives the reference-format .bwt.2bit.64 file. */
 int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, const char *out_path,
                        gb_fmi_index **out);
+/* Builds the search-side Occ32 table now (otherwise the first search does); call it before host
+ * threads share the index. */
+int gb_fmi_index_prepare(gb_fmi_index *idx);
 /* n = reference_seq_len (|text|+1), count[5] as used by the search (load-time +1 applied). */
 int gb_fmi_index_info(gb_fmi_index *idx, int64_t *n, int64_t *count5, int64_t *sentinel_index);
 /* Copies the CP_OCC table (64 bytes per 64 BWT rows, reference layout) to host memory. */
@@ -95,6 +98,37 @@ int gb_fmi_reads_sa_results(gb_fmi_reads *r, int64_t *coords, int64_t coords_cap
                             int64_t *total);
 /* Kernel time of the last SA run (row expansion + LF walks, HIP events), LF steps taken, coordinates. */
 int gb_fmi_reads_sa_timing(gb_fmi_reads *r, float *ms, int64_t *lf_steps, int64_t *coords);
+
+/* ---- Per-call phases (the FMI_search method adapter, include/gb_compat/FMI_search.h). Reads are
+ * addressed like the reference: read r = enc_qdb[offs[r] .. offs[r] + lens[r]) (offs =
+ * query_cum_len_ar, lens = seq_[r].l_seq) for r in [0, nrid). Output goes to out[0 .. *nout) in the
+ * reference's emission order (out may be NULL to only count); bwt_calls (nullable) = backwardExt calls.
+ * Synchronous; each host thread uses its own stream and device buffers on the index's device. */
+/* getSMEMsOnePosOneThread (FMI_search.cpp:986-1180): task t = read rid[t] from query_pos[t] with
+ * min_intv[t]; next_pos[t] (nullable) receives the updated query position. */
+int gb_fmi_smem_onepos(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                       int32_t nrid, const int16_t *query_pos, const int32_t *min_intv, const int32_t *rid,
+                       int32_t ntasks, int32_t min_seed_len, gb_smem *out, int64_t out_cap, int64_t *nout,
+                       int16_t *next_pos, int64_t *bwt_calls);
+/* getSMEMsAllPosOneThread (FMI_search.cpp:1182-1241): task t = read rid[t] at every x start with
+ * min_intv[t], output round-major like the reference's do-while; rounds[t] (nullable) = the number of
+ * x starts of task t (what the caller-visible compaction of rid/min_intv depends on). */
+int gb_fmi_smem_allpos(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                       int32_t nrid, const int32_t *min_intv, const int32_t *rid, int32_t ntasks,
+                       int32_t min_seed_len, gb_smem *out, int64_t out_cap, int64_t *nout, int32_t *rounds,
+                       int64_t *bwt_calls);
+/* bwtSeedStrategyAllPosOneThread (FMI_search.cpp:1243-1326): reads 0..nreads-1 with max_intv[i]; SMEM
+ * rid = i. */
+int gb_fmi_last_seeds(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
+                      int32_t nreads, const int32_t *max_intv, int32_t min_seed_len, gb_smem *out, int64_t out_cap,
+                      int64_t *nout, int64_t *bwt_calls);
+
+/* get_sa_entry / get_sa_entries(pos[]) (FMI_search.cpp:1566-1586): the raw sampled-SA entries at
+ * indices pos[i] (0 <= pos < (n >> 3) + 1, sa_ms_byte << 32 + sa_ls_word). */
+int gb_fmi_sa_raw(gb_fmi_index *idx, const int64_t *pos, int64_t n, int64_t *out);
+/* call_one_step (FMI_search.cpp:1834-1893): one LF step from row pos; *done = the reference's return
+ * value (1: *sa_entry is final), *offset updated like the reference's reference argument. */
+int gb_fmi_sa_one_step(gb_fmi_index *idx, int64_t pos, int64_t *sa_entry, int64_t *offset, int32_t *done);
 
 /* Diagnostic: per-wave clock sums of the search kernel's phases when GB_FMI_FLAGS has bit 2 (value
  * 4) set -- out = {state machine, gather wait, consume, trips, lane state-loop iterations, trips in

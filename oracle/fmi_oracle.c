@@ -537,6 +537,25 @@ int64_t fmi_oracle_run(or_fmi *f, const uint8_t *enc_qdb, const int32_t *lens, i
   return total;
 }
 
+/* One phase of the class API in the reference's own emission order (test infrastructure for the
+ * FMI_search method adapter): phase 0 getSMEMsAllPosOneThread (rid/intv compacted in place like the
+ * reference), 1 getSMEMsOnePosOneThread (qpos updated in place), 2 bwtSeedStrategyAllPosOneThread
+ * (intv = max_intv, reads 0..num-1). Returns the number of SMEMs written to out. */
+int64_t fmi_oracle_phase(or_fmi *f, int phase, const uint8_t *qdb, const int32_t *lens, const int32_t *cum,
+                         int16_t *qpos, int32_t *intv, int32_t *rid, int32_t num, int32_t max_readlength,
+                         int32_t minSeedLen, or_smem *out) {
+  or_smem *prev = (or_smem *)malloc((size_t)(max_readlength + 1) * sizeof(or_smem));
+  int64_t nt = 0;
+  if (phase == 0)
+    smems_all_pos(f, qdb, intv, rid, num, lens, cum, minSeedLen, out, &nt, prev);
+  else if (phase == 1)
+    smems_one_pos(f, qdb, qpos, intv, rid, num, lens, cum, minSeedLen, out, &nt, prev);
+  else
+    nt = seed_strategy(f, qdb, intv, num, lens, cum, minSeedLen, out);
+  free(prev);
+  return nt;
+}
+
 /* ctypes-friendly handle API */
 or_fmi *fmi_oracle_new(void) { return (or_fmi *)calloc(1, sizeof(or_fmi)); }
 void fmi_oracle_delete(or_fmi *f) {

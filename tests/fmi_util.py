@@ -342,3 +342,43 @@ def check_index_structure(ref, n, count5, sentinel, cp_occ, sa_sampled=None, sam
     assert (bwt_char(cp_occ, rows) == exp).all(), "BWT[row] != text[SA[row] - 1]"
     t2 = t[t + 1 < ns]
     assert suffix_less(text, sa[t2], sa[t2 + 1]).all(), "sampled SA rows out of suffix order"
+
+
+def read_index_file(path):
+    """(n, count5 as stored, cp_occ int64[rows, 8], packed sampled SA int64, sentinel) of a
+    .bwt.2bit.64 file (layout of build_fm_index, FMI_search.cpp:171-356)."""
+    raw = np.fromfile(path, np.uint8)
+    n = int(raw[:8].view(np.int64)[0])
+    count5 = raw[8:48].view(np.int64).copy()
+    sz = (n >> 6) + 1
+    o = 48
+    cp = raw[o:o + sz * 64].view(np.int64).reshape(sz, 8)
+    o += sz * 64
+    ns = (n >> 3) + 1
+    ms = raw[o:o + ns].view(np.int8).astype(np.int64)
+    ls = raw[o + ns:o + 5 * ns].view(np.uint32).astype(np.int64)
+    sentinel = int(raw[o + 5 * ns:o + 5 * ns + 8].view(np.int64)[0])
+    return n, count5, cp, (ms << 32) | ls, sentinel
+
+
+def call_one_step(n_count5_loaded, cp, sa, pos, offset=0):
+    """call_one_step (FMI_search.cpp:1834-1893) restated over the file tables: (ret, sa_entry, offset)."""
+    if pos & 7 == 0:
+        return 1, int(sa[pos >> 3]), offset
+    line = cp[pos >> 6]
+    y = 63 - (pos & 63)
+    b = 4
+    for c in range(4):
+        if (int(line[4 + c]) >> y) & 1:
+            b = c
+            break
+    if b == 4:
+        return 1, 0, offset
+    yy = pos & 63
+    mask = ((1 << 64) - 1) ^ ((1 << (64 - yy)) - 1) if yy else 0
+    occ = int(line[b]) + bin((int(line[4 + b]) & ((1 << 64) - 1)) & mask).count("1")
+    sp = int(n_count5_loaded[b]) + occ
+    offset += 1
+    if sp & 7 == 0:
+        return 1, int(sa[sp >> 3]) + offset, offset
+    return 0, sp, offset
