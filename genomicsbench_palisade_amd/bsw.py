@@ -144,3 +144,16 @@ def get_scores16(pairs, params=None):
     check(_decl().gb_bsw_get_scores16(ctypes.byref(params), _buf(sp), pairs.n, _buf(pairs.tgt), len(pairs.tgt),
                                       _buf(pairs.qry), len(pairs.qry)), "gb_bsw_get_scores16")
     return sp
+
+
+def get_scores8(pairs, params=None, w_match: int = 1):
+    """One-shot getScores8 (the 8-bit path's domain only: len1, len2 < 128, h0 + min(len1, len2) *
+    w_match < 128, bwamem.cpp:2152-2155; raises GbError for any other pair)."""
+    params = params if params is not None else default_params()
+    sp = seqpairs(pairs)
+    L = _decl()
+    L.gb_bsw_get_scores8.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    check(L.gb_bsw_get_scores8(ctypes.byref(params), w_match, _buf(sp), pairs.n, _buf(pairs.tgt), len(pairs.tgt),
+                               _buf(pairs.qry), len(pairs.qry), None), "gb_bsw_get_scores8")
+    return sp

@@ -885,4 +885,24 @@ int gb_bsw_get_scores16(const gb_bsw_params *params, gb_seqpair *pairs, int64_t 
   return gb_bsw_get_scores16_ex(params, pairs, n, ref, ref_bytes, qer, qer_bytes, nullptr);
 }
 
+// getScores8 (bandedSWA.cpp:426-725, smithWaterman256_8 :727-1123): the reference's 8-bit kernel
+// keeps every score in int8 lanes and is only defined where nothing wraps; its own caller in bwa-mem2
+// sends a pair to it iff len1 < 128, len2 < 128 and h0 + min(len1, len2) * a < 128
+// (tools/bwa-mem2/src/bwamem.cpp:2152-2155, MAX_SEQ_LEN8 = 128). Inside that domain the 8-bit kernel
+// is the 16-bit DP, so those pairs run the exact kernel; a pair outside it is refused loudly (the
+// reference asserts on len2, bandedSWA.cpp:607-608, and wraps silently otherwise).
+int gb_bsw_get_scores8(const gb_bsw_params *params, int32_t w_match, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
+                       int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes, int64_t *total_cells) {
+  GB_ARG(params && (n == 0 || pairs), "gb_bsw_get_scores8: null argument");
+  for (int64_t i = 0; i < n; i++) {
+    const gb_seqpair &p = pairs[i];
+    const int64_t minval = (int64_t)p.h0 + (int64_t)std::min(p.len1, p.len2) * w_match;
+    GB_ARG(p.len1 < 128 && p.len2 < 128 && p.len1 >= 0 && p.len2 >= 0 && minval < 128,
+           "gb_bsw_get_scores8: pair %lld (len1 %d, len2 %d, h0 %d) is outside the 8-bit kernel's domain "
+           "(len1 < 128, len2 < 128, h0 + min(len1, len2) * %d < 128; bwamem.cpp:2152-2155): use getScores16",
+           (long long)i, p.len1, p.len2, p.h0, w_match);
+  }
+  return gb_bsw_get_scores16_ex(params, pairs, n, ref, ref_bytes, qer, qer_bytes, total_cells);
+}
+
 }  // extern "C"

@@ -36,8 +36,8 @@ static void ensure_device() {
 
 BandedPairWiseSW::BandedPairWiseSW(const int o_del, const int e_del, const int o_ins, const int e_ins,
                                    const int zdrop, const int end_bonus, const int8_t *mat_,
-                                   const int8_t /*w_match*/, const int8_t /*w_mismatch*/, int /*numThreads*/)
-    : SW_cells(0), ticks_(0) {
+                                   const int8_t w_match, const int8_t /*w_mismatch*/, int /*numThreads*/)
+    : SW_cells(0), ticks_(0), w_match_(w_match) {
   std::memset(&p_, 0, sizeof(p_));
   p_.o_del = o_del;
   p_.e_del = e_del;
@@ -76,9 +76,21 @@ void BandedPairWiseSW::getScores16(SeqPair *pairArray, uint8_t *seqBufRef, uint8
   ticks_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// getScores8: exact results for the pairs the 8-bit kernel is defined on (gb_bsw_get_scores8); a pair
+// outside that domain aborts, as the reference's assert on len2 does (bandedSWA.cpp:607-608).
 void BandedPairWiseSW::getScores8(SeqPair *pairArray, uint8_t *seqBufRef, uint8_t *seqBufQer, int32_t numPairs,
-                                  uint16_t numThreads, int32_t w) {
-  getScores16(pairArray, seqBufRef, seqBufQer, numPairs, numThreads, w);
+                                  uint16_t /*numThreads*/, int32_t w) {
+  ensure_device();
+  const auto t0 = std::chrono::steady_clock::now();
+  gb_bsw_params p = p_;
+  p.w = w;
+  int64_t cells = 0;
+  const int st = gb_bsw_get_scores8(&p, w_match_, gbp(pairArray), numPairs, seqBufRef,
+                                    span_end(pairArray, numPairs, true), seqBufQer,
+                                    span_end(pairArray, numPairs, false), &cells);
+  if (st) die("gb_bsw_get_scores8", st);
+  SW_cells += (uint64_t)cells;
+  ticks_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
 int BandedPairWiseSW::scalarBandedSWA(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int32_t w,

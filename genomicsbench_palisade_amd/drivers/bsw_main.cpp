@@ -18,7 +18,7 @@
 #include "../../include/gb_compat/bandedSWA.h"
 
 int main(int argc, char **argv) {
-  int w_match = 1, w_mismatch = 4, w_open = 6, w_extend = 1, w_ambig = -1, threads = 1, batch = 0;
+  int w_match = 1, w_mismatch = 4, w_open = 6, w_extend = 1, w_ambig = -1, threads = 1, batch = 0, bits = 16;
   const char *pair_file = nullptr, *out_file = nullptr;
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!strcmp(argv[i], "-match")) w_match = atoi(argv[i + 1]);
@@ -30,6 +30,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "-t")) threads = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "-b")) batch = atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "-o")) out_file = argv[i + 1];
+    else if (!strcmp(argv[i], "-bits")) bits = atoi(argv[i + 1]);  // 8: getScores8 (bwa-mem2's 8-bit path)
     // -h0 is parsed by the reference but unused: every pair carries its own h0 line
   }
   if (!pair_file) {
@@ -92,7 +93,9 @@ int main(int argc, char **argv) {
                        (int8_t)w_mismatch, threads);
   (void)batch;
   const auto t0 = std::chrono::steady_clock::now();
-  if (!pairs.empty())
+  if (!pairs.empty() && bits == 8)
+    bsw.getScores8(pairs.data(), ref.data(), qer.data(), (int32_t)pairs.size(), (uint16_t)threads, w);
+  else if (!pairs.empty())
     bsw.getScores16(pairs.data(), ref.data(), qer.data(), (int32_t)pairs.size(), (uint16_t)threads, w);
   const double sw_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   printf("Executed MI355X banded SW (gfx950)...\n");

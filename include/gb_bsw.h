@@ -78,6 +78,13 @@ int gb_bsw_get_scores16(const gb_bsw_params *params, gb_seqpair *pairs, int64_t 
 int gb_bsw_get_scores16_ex(const gb_bsw_params *params, gb_seqpair *pairs, int64_t num_pairs,
                            const uint8_t *seq_buf_ref, int64_t ref_bytes, const uint8_t *seq_buf_qer,
                            int64_t qer_bytes, int64_t *total_cells);
+/* getScores8 (bandedSWA.cpp:426-725): the 8-bit kernel's domain is the one its bwa-mem2 caller
+ * routes to it (bwamem.cpp:2152-2155): len1 < 128, len2 < 128, h0 + min(len1, len2) * w_match < 128.
+ * Pairs in it get the exact (16-bit) results; any pair outside it fails the call with GB_ERR_ARG and
+ * nothing is written. */
+int gb_bsw_get_scores8(const gb_bsw_params *params, int32_t w_match, gb_seqpair *pairs, int64_t num_pairs,
+                       const uint8_t *seq_buf_ref, int64_t ref_bytes, const uint8_t *seq_buf_qer,
+                       int64_t qer_bytes, int64_t *total_cells);
 
 #ifdef __cplusplus
 }

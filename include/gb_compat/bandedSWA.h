@@ -9,7 +9,8 @@
  *   getScores8, getTicks               getTicks (bandedSWA.cpp:110-124)
  * Implemented by genomicsbench_palisade_amd/lib/libgb_bsw_dropin.so (csrc/bsw_dropin.cpp): every
  * call runs csrc/bsw.hip on the device selected by $GB_DEVICE (default 0). numThreads is accepted
- * and ignored. getScores8 has getScores16's semantics (exact for scores that fit the 8-bit path).
+ * and ignored. getScores8 computes the pairs of the 8-bit kernel's domain (len1, len2 < 128 and
+ * h0 + min(len1, len2) * w_match < 128, bwamem.cpp:2152-2155) exactly and aborts on any other pair.
  */
 #ifndef GB_COMPAT_BANDEDSWA_H
 #define GB_COMPAT_BANDEDSWA_H
@@ -63,6 +64,7 @@ class BandedPairWiseSW {
  private:
   gb_bsw_params p_;
   int64_t ticks_;
+  int32_t w_match_;
 };
 
 #endif

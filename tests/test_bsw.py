@@ -180,3 +180,70 @@ def test_gpu_cli_dropin(golden, tmp_path):
     assert f"Total Pairs processed: {p.n}" in r.stdout
     got = np.loadtxt(fout, dtype=np.int32, ndmin=2)
     assert_same(got, exp, "bsw CLI")
+
+
+def reference_outputs(p, P):
+    """ksw_extend2 from the reference tree when built (oracle/_ref), else the restatement."""
+    lib = oracle_lib.ref_bsw()
+    return oracle_lib.ref_bsw_run(lib, p, P) if lib is not None else oracle_lib.bsw_oracle(p, P)[0]
+
+
+def outs_of(sp):
+    return np.stack([sp[f] for f in FIELDS], axis=1)
+
+
+def eight_bit_pairs(n, seed):
+    """Pairs inside the 8-bit kernel's domain (bwamem.cpp:2152-2155): len1, len2 < 128 and
+    h0 + min(len1, len2) < 128 (match score 1), including the boundary values."""
+    p = gen.bsw_pairs(n, seed=seed, qlen=(1, 120), extra=(0, 7))
+    h0 = p.h0.copy()
+    lim = 127 - np.minimum(p.tlen, p.qlen)
+    h0 = np.minimum(h0, lim).astype(np.int32)
+    h0[::7] = lim[::7]  # h0 + min(len1, len2) == 127
+    return gen.BswPairs(p.tgt, p.toff, p.tlen, p.qry, p.qoff, p.qlen, h0)
+
+
+@pytest.mark.gpu
+def test_gpu_scores8_domain_exact_and_refusal():
+    """getScores8 (bandedSWA.cpp:426-725): pairs of the 8-bit domain are bit-exact against the reference
+    ksw_extend2 (and the 16-bit path); a call holding one pair outside the domain is refused and writes
+    nothing."""
+    from genomicsbench_palisade_amd import GbError, set_device
+    set_device(0)
+    p = eight_bit_pairs(6000, 71)
+    assert p.tlen.max() < 128 and p.qlen.max() < 128
+    params = bsw.default_params()
+    exp = reference_outputs(p, params)
+    sp = bsw.get_scores8(p, params)
+    assert_same(outs_of(sp), exp, "getScores8")
+    for bad in ("len1", "len2", "h0"):
+        q = p.subset(np.arange(50))
+        if bad == "len1":
+            q = gen.concat_bsw([q, gen.bsw_pairs(1, seed=3, qlen=(20, 20), extra=(110, 110))])
+        elif bad == "len2":
+            q = gen.concat_bsw([q, gen.bsw_pairs(1, seed=3, qlen=(128, 128), extra=(0, 0))])
+        else:
+            q.h0 = q.h0.copy()
+            q.h0[10] = 128 - min(int(q.tlen[10]), int(q.qlen[10]))
+        with pytest.raises(GbError, match="8-bit"):
+            bsw.get_scores8(q, params)
+
+
+@pytest.mark.gpu
+def test_gpu_cli_scores8(tmp_path):
+    """bin/bsw -bits 8 runs BandedPairWiseSW::getScores8 of the drop-in on a loadPairs file."""
+    import subprocess
+    from conftest import ROOT
+    p = eight_bit_pairs(3000, 72)
+    exp = reference_outputs(p, bsw.default_params())
+    fin, fout = tmp_path / "pairs.txt", tmp_path / "out.tsv"
+    gen.write_bsw_file(fin, p)
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "bsw")
+    r = subprocess.run([exe, "-pairs", str(fin), "-t", "1", "-b", "512", "-bits", "8", "-o", str(fout)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert_same(np.loadtxt(fout, dtype=np.int32, ndmin=2), exp, "bsw CLI -bits 8")
+    bad = gen.bsw_pairs(20, seed=5, qlen=(130, 140))
+    gen.write_bsw_file(fin, bad)
+    r = subprocess.run([exe, "-pairs", str(fin), "-bits", "8"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "8-bit" in r.stderr
