@@ -345,6 +345,55 @@ def shard_note(args, what: str, lo: int, hi: int, total: int, world: int) -> str
     return f"{total} {what} per rank (own seed)"
 
 
+def e2e_time(fn, reps: int = 2) -> float:
+    """Mean wall seconds of fn() over `reps` calls after one warm call (host arrays in, host arrays out)."""
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps
+
+
+def phmm_dropin_e2e(args, D, ta, cells, rank, world):
+    """The reference's entry point itself, end to end: computelikelihoodsboth (the GKL C++ symbol of
+    lib/libgkl_pairhmm_c.so, IntelPairHmmCSource.cpp:61-85) over the rank's testcases as host arrays --
+    pack, H2D, f32 + f64 kernels, D2H, log10 -- and, on one GPU, bin/phmm (PairHMMUnitTest.cpp's CLI)
+    parsing a large-shaped .in file of the same job."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "genomicsbench_palisade_amd", "lib", "libgkl_pairhmm_c.so"))
+    both = getattr(lib, "_Z22computelikelihoodsbothP8testcasePdi")
+    both.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    getattr(lib, "_Z11initPairHMMv")()
+    out = np.zeros(max(ta.n, 1))
+    D.barrier()
+    t = D.max(e2e_time(lambda: both(ctypes.addressof(ta.arr), out.ctypes.data, ta.n)))
+    res = {"computelikelihoodsboth": {"value": D.sum(float(cells)) / t / 1e9, "unit": "GCUPS", "seconds": t,
+                                      "note": "host testcase[] in, double[] out: pack + H2D + kernels + D2H + log10"}}
+    return res
+
+
+def phmm_cli_e2e(batches, cells):
+    """bin/phmm -f <large-shaped .in> -t 1 (whole job, one GPU): wall time incl. parsing and its own
+    'Kernel runtime' line (pack + H2D + compute + D2H, no parsing)."""
+    import subprocess
+    import tempfile
+    from genomicsbench_palisade_amd import gen
+    exe = os.path.join(ROOT, "genomicsbench_palisade_amd", "bin", "phmm")
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "large.in")
+        gen.write_phmm_file(f, batches)
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "-f", f, "-t", "1"], capture_output=True, text=True, timeout=600)
+        wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    rt = [float(ln.split(":")[1].split()[0]) for ln in r.stdout.splitlines() if "Kernel runtime" in ln]
+    kr = rt[0] if rt else float("nan")
+    return {"value": cells / kr / 1e9 if kr > 0 else None, "unit": "GCUPS", "kernel_runtime_s": kr, "wall_s": wall,
+            "wall_gcups": cells / wall / 1e9,
+            "note": "bin/phmm on the job written as a .in file: 'Kernel runtime' (pack, H2D, kernels, D2H) and "
+                    "process wall time (file parsing + runtime start-up included)"}
+
+
 def bench_chain(args, D, rank, world, kind="large"):
     from genomicsbench_palisade_amd import chain, gen, shard
     log(f"chain {kind}: generating calls")
@@ -388,6 +437,20 @@ def bench_chain(args, D, rank, world, kind="large"):
             cpu = cpu_baseline_chain(calls, args.cpu_seconds)
         out["cpu_baseline"] = cpu
         out["backtrack"] = bench_chain_backtrack(args, D, rank, world, b, calls)
+        if not args.no_e2e:
+            log("chain: drop-in end to end")
+            from genomicsbench_palisade_amd import check, lib
+            L = lib()
+            outs = [np.zeros(max(calls.nanchors, 1), np.int32) for _ in range(4)]
+            t = D.max(e2e_time(lambda: check(L.gb_chain(
+                ctypes.c_int64(calls.ncalls), calls.offsets.ctypes.data_as(ctypes.c_void_p),
+                calls.avg_qspan.ctypes.data_as(ctypes.c_void_p), calls.params4.ctypes.data_as(ctypes.c_void_p),
+                calls.x.ctypes.data_as(ctypes.c_void_p), calls.y.ctypes.data_as(ctypes.c_void_p),
+                *[o.ctypes.data_as(ctypes.c_void_p) for o in outs]), "gb_chain")))
+            out["dropin_e2e"] = {"gb_chain": {
+                "value": anchors_all / t / 1e6, "unit": "Manchors/s", "seconds": t,
+                "note": "host_chain_kernel's C ABI over the rank's calls in CSR: H2D + chain_dp + D2H of "
+                        "score/parent/target/peak (the C++ drop-in adds the std::vector copies)"}}
     b.close()
     return out
 
@@ -488,6 +551,18 @@ def bench_bsw(args, D, rank, world, kind="large"):
             log("bsw: CPU baseline")
             cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds)
         out["cpu_baseline"] = cpu
+        if not args.no_e2e:
+            log("bsw: drop-in end to end")
+            b.close()
+            sp = bsw.seqpairs(pairs)
+            L = bsw._decl()
+            t = D.max(e2e_time(lambda: bsw.check(L.gb_bsw_get_scores16(
+                ctypes.byref(params), bsw._buf(sp), pairs.n, bsw._buf(pairs.tgt), len(pairs.tgt), bsw._buf(pairs.qry),
+                len(pairs.qry)), "gb_bsw_get_scores16")))
+            out["dropin_e2e"] = {"gb_bsw_get_scores16": {
+                "value": cells_all / t / 1e9, "unit": "GCUPS", "seconds": t,
+                "note": "BandedPairWiseSW::getScores16's C ABI over the rank's SeqPair[] and sequence buffers: "
+                        "H2D + kernels + D2H into the SeqPair array"}}
     b.close()
     return out
 
@@ -552,6 +627,13 @@ def bench_phmm(args, D, rank, world, kind="large"):
             log("phmm: CPU baseline")
             cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
         out["cpu_baseline"] = cpu
+        if not args.no_e2e:
+            log("phmm: drop-in end to end")
+            job.close()
+            e2e = phmm_dropin_e2e(args, D, ta, cells, rank, world)
+            if world == 1:
+                e2e["bin/phmm"] = phmm_cli_e2e(batches, full.cells())
+            out["dropin_e2e"] = e2e
     job.close()
     return out
 
@@ -601,6 +683,19 @@ def bench_fmi(args, D, rank, world):
         log("fmi: CPU baseline")
         cpu = cpu_baseline_fmi(oi, codes, lens, args.cpu_seconds, fmi, idx)
         oi.close()
+    e2e = None
+    if not args.no_e2e:
+        log("fmi: drop-in end to end")
+
+        def once():
+            r2 = fmi.Reads(idx, codes, lens)
+            r2.search(19)
+            r2.results(batch_size=512)
+            r2.close()
+        t = D.max(e2e_time(once, reps=1))
+        e2e = {"gb_fmi_search": {"value": reads_all / t / 1e6, "unit": "Mreads/s", "seconds": t,
+                                 "note": "enc_qdb + lengths H2D, fmi.cpp batch pipeline, all SMEMs + per-batch "
+                                         "counts D2H (index already resident)"}}
     sa = bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens)
     rs.close()
     small = bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref)
@@ -622,6 +717,7 @@ def bench_fmi(args, D, rank, world):
                      "occ32_bytes": int(occ_bytes), "achieved_occ32": occ_bytes / (ms * 1e-3) / 1e9},
         "kernels_ms": {"smem_search": ms},
         "cpu_baseline": cpu,
+        "dropin_e2e": e2e,
         "sa_lookup": sa,
         "small": small,
     }
@@ -740,6 +836,7 @@ def main():
     ap.add_argument("--no-small", action="store_true", help="skip the 'small'-set legs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end (host arrays) timings")
     args = ap.parse_args()
 
     world, rank, local = dist_env()

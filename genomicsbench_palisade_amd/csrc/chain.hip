@@ -412,52 +412,106 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
 
 }  // namespace gbchain
 
-extern "C" {
 
-int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
-                          const int32_t *params4, const uint64_t *x, const uint64_t *y,
-                          gb_chain_batch **out) {
-  GB_ARG(out && ncalls >= 0 && offsets, "gb_chain_batch_create: bad arguments");
-  GB_ARG(ncalls < (1ll << 31), "gb_chain_batch_create: too many calls");
-  *out = nullptr;
+namespace {
+// A CSR call set the kernel can take (checked before any device work).
+int validate(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
+             const uint64_t *x, const uint64_t *y) {
+  GB_ARG(ncalls >= 0 && offsets, "gb_chain: bad arguments");
+  GB_ARG(ncalls < (1ll << 31), "gb_chain: too many calls");
   const int64_t na = offsets[ncalls];
-  GB_ARG(offsets[0] == 0 && na >= 0 && (na == 0 || (x && y)), "gb_chain_batch_create: bad offsets");
+  GB_ARG(offsets[0] == 0 && na >= 0 && (na == 0 || (x && y)), "gb_chain: bad offsets");
   for (int64_t c = 0; c < ncalls; c++)
     GB_ARG(offsets[c + 1] >= offsets[c] && offsets[c + 1] - offsets[c] < (1ll << 30),
-           "gb_chain_batch_create: call %lld has a bad anchor range", (long long)c);
-  GB_ARG(ncalls == 0 || (avg_qspan && params4), "gb_chain_batch_create: null parameters");
+           "gb_chain: call %lld has a bad anchor range", (long long)c);
+  GB_ARG(ncalls == 0 || (avg_qspan && params4), "gb_chain: null parameters");
+  return GB_OK;
+}
+
+// Uploads a validated call set into B, growing B's buffers only when they are too small.
+int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
+               const int32_t *params4, const uint64_t *x, const uint64_t *y) {
+  if (int st = validate(ncalls, offsets, avg_qspan, params4, x, y)) return st;
+  const int64_t na = offsets[ncalls];
   // longest calls first: the grid is dispatched in order, so the critical path starts first
   std::vector<int32_t> order((size_t)ncalls);
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
     return offsets[a + 1] - offsets[a] > offsets[b + 1] - offsets[b];
   });
-  auto *B = new gb_chain_batch();
+  GB_HIP(hipSetDevice(B->device));
+  GB_HIP(hipStreamSynchronize(B->stream));  // the previous contents may still be in use
+  gbchain::chain_bt_destroy(B->bt);
+  B->bt = nullptr;
+  B->ran = false;
+  const int64_t nc = std::max<int64_t>(ncalls, 1), nn = std::max<int64_t>(na, 1);
+  if (nc > B->cap_calls) {
+    for (void *q : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order}) (void)hipFree(q);
+    B->d_off = nullptr, B->d_aq = nullptr, B->d_par4 = nullptr, B->d_order = nullptr;
+    B->cap_calls = 0;
+    GB_HIP(hipMalloc(&B->d_off, (size_t)(nc + 1) * sizeof(int64_t)));
+    GB_HIP(hipMalloc(&B->d_aq, (size_t)nc * sizeof(float)));
+    GB_HIP(hipMalloc(&B->d_par4, (size_t)nc * 4 * sizeof(int32_t)));
+    GB_HIP(hipMalloc(&B->d_order, (size_t)nc * sizeof(int32_t)));
+    B->cap_calls = nc;
+  }
+  if (nn > B->cap_anchors) {
+    for (void *q : {(void *)B->d_x, (void *)B->d_y, (void *)B->d_out}) (void)hipFree(q);
+    B->d_x = nullptr, B->d_y = nullptr, B->d_out = nullptr;
+    B->cap_anchors = 0;
+    GB_HIP(hipMalloc(&B->d_x, (size_t)nn * sizeof(uint64_t)));
+    GB_HIP(hipMalloc(&B->d_y, (size_t)nn * sizeof(uint64_t)));
+    GB_HIP(hipMalloc(&B->d_out, (size_t)nn * 4 * sizeof(int32_t)));
+    B->cap_anchors = nn;
+  }
   B->ncalls = ncalls;
   B->nanchors = na;
+  GB_HIP(hipMemcpy(B->d_off, offsets, (size_t)(ncalls + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (ncalls) {
+    GB_HIP(hipMemcpy(B->d_aq, avg_qspan, (size_t)ncalls * sizeof(float), hipMemcpyHostToDevice));
+    GB_HIP(hipMemcpy(B->d_par4, params4, (size_t)ncalls * 16, hipMemcpyHostToDevice));
+    GB_HIP(hipMemcpy(B->d_order, order.data(), (size_t)ncalls * 4, hipMemcpyHostToDevice));
+  }
+  if (na) {
+    GB_HIP(hipMemcpy(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice));
+    GB_HIP(hipMemcpy(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice));
+  }
+  return GB_OK;
+}
+
+int batch_new(gb_chain_batch **out) {
+  auto *B = new gb_chain_batch();
   hipError_t e = hipGetDevice(&B->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
   for (auto &ev : B->ev)
     if (e == hipSuccess) e = hipEventCreate(&ev);
-  const size_t nc = (size_t)std::max<int64_t>(ncalls, 1), nn = (size_t)std::max<int64_t>(na, 1);
-  if (e == hipSuccess) e = hipMalloc(&B->d_off, (nc + 1) * sizeof(int64_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_aq, nc * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&B->d_par4, nc * 4 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_order, nc * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_x, nn * sizeof(uint64_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_y, nn * sizeof(uint64_t));
-  if (e == hipSuccess) e = hipMalloc(&B->d_out, nn * 4 * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&B->d_vis, sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemcpy(B->d_off, offsets, (size_t)(ncalls + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_aq, avg_qspan, (size_t)ncalls * sizeof(float), hipMemcpyHostToDevice);
-  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_par4, params4, (size_t)ncalls * 16, hipMemcpyHostToDevice);
-  if (e == hipSuccess && ncalls) e = hipMemcpy(B->d_order, order.data(), (size_t)ncalls * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess && na) e = hipMemcpy(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess && na) e = hipMemcpy(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
-    gb::set_error("gb_chain_batch_create: %s", hipGetErrorString(e));
+    gb::set_error("gb_chain: %s", hipGetErrorString(e));
     gb_chain_batch_destroy(B);
     return GB_ERR_HIP;
+  }
+  *out = B;
+  return GB_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
+                          const int32_t *params4, const uint64_t *x, const uint64_t *y,
+                          gb_chain_batch **out) {
+  GB_ARG(out, "gb_chain_batch_create: null out");
+  *out = nullptr;
+  int st = validate(ncalls, offsets, avg_qspan, params4, x, y);
+  if (st) return st;
+  gb_chain_batch *B = nullptr;
+  st = batch_new(&B);
+  if (st) return st;
+  st = batch_fill(B, ncalls, offsets, avg_qspan, params4, x, y);
+  if (st) {
+    gb_chain_batch_destroy(B);
+    return st;
   }
   *out = B;
   return GB_OK;
@@ -567,12 +621,24 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
 int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
              const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents, int32_t *targets,
              int32_t *peak_scores) {
-  gb_chain_batch *B = nullptr;
-  int st = gb_chain_batch_create(ncalls, offsets, avg_qspan, params4, x, y, &B);
+  // one cached batch per (host thread, device): repeated host_chain_kernel calls reuse its stream,
+  // events and grow-only buffers. Never freed (freeing at thread exit could run after the HIP
+  // runtime is torn down).
+  int st = validate(ncalls, offsets, avg_qspan, params4, x, y);
   if (st) return st;
+  thread_local std::vector<std::pair<int, gb_chain_batch *>> ws;
+  int dev = 0;
+  GB_HIP(hipGetDevice(&dev));
+  gb_chain_batch *B = nullptr;
+  for (auto &w : ws)
+    if (w.first == dev) B = w.second;
+  if (!B) {
+    if ((st = batch_new(&B))) return st;
+    ws.emplace_back(dev, B);
+  }
+  if ((st = batch_fill(B, ncalls, offsets, avg_qspan, params4, x, y))) return st;
   st = gb_chain_batch_run(B);
   if (!st) st = gb_chain_batch_results(B, scores, parents, targets, peak_scores, nullptr);
-  gb_chain_batch_destroy(B);
   return st;
 }
 

@@ -14,6 +14,7 @@ struct gb_chain_batch {
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t ncalls = 0, nanchors = 0;
+  int64_t cap_calls = 0, cap_anchors = 0;  // allocated sizes (a refilled batch reuses its buffers)
   int64_t *d_off = nullptr;
   float *d_aq = nullptr;
   int32_t *d_par4 = nullptr, *d_order = nullptr;
