@@ -30,7 +30,7 @@ $(LIB)/obj/gb_common.o: $(CSRC)/gb_common.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB)/libgb.so: $(HIP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 
 # Reference-compatible drop-in: exports initPairHMM()/computelikelihoodsboth() with the reference's
 # C++ linkage (IntelPairHmmCSource.cpp:29-115) on top of libgb.so.

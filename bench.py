@@ -889,6 +889,7 @@ def main():
             "roofline_f64": ph["roofline_f64"] if ph else None,
             "kernels_ms": ph["kernels_ms"] if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
+            "dropin_e2e": ph.get("dropin_e2e") if ph else None,
             "fmi": fm,
             "chain": ch,
             "bsw": bw,

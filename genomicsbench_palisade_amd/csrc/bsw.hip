@@ -714,6 +714,7 @@ int gb_bsw_batch_create(const gb_bsw_params *params, const gb_seqpair *pairs, in
 }
 
 int gb_bsw_batch_run(gb_bsw_batch *B) {
+  gb::Range range_("gb.bsw.batch_run");
   GB_ARG(B, "gb_bsw_batch_run: null batch");
   GB_HIP(hipSetDevice(B->device));
   GB_HIP(hipMemsetAsync(B->d_total, 0, 2 * sizeof(unsigned long long), B->stream));
@@ -860,6 +861,7 @@ int gb_bsw_batch_timing(gb_bsw_batch *B, float *kernel_ms) {
 
 int gb_bsw_get_scores16_ex(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
                            int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes, int64_t *total_cells) {
+  gb::Range range_("gb.bsw.get_scores16");
   // one cached batch per (host thread, device): the reference calls getScores16 once per batch of
   // 512 pairs (main_banded.cpp:896-909), so streams, events and buffers are reused across calls.
   // Never freed (freeing at thread exit could run after the HIP runtime is torn down).

@@ -518,6 +518,7 @@ int gb_chain_batch_create(int64_t ncalls, const int64_t *offsets, const float *a
 }
 
 int gb_chain_batch_run(gb_chain_batch *B) {
+  gb::Range range_("gb.chain.batch_run");
   GB_ARG(B, "gb_chain_batch_run: null batch");
   GB_HIP(hipSetDevice(B->device));
   GB_HIP(hipMemsetAsync(B->d_vis, 0, sizeof(unsigned long long), B->stream));

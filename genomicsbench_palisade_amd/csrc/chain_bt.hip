@@ -502,6 +502,7 @@ int bt_alloc(gb_chain_batch *B) {
 extern "C" {
 
 int gb_chain_batch_backtrack(gb_chain_batch *B, int32_t min_cnt, int32_t min_sc) {
+  gb::Range range_("gb.chain.backtrack");
   GB_ARG(B && B->ran, "gb_chain_batch_backtrack: chain_dp has not run on this batch");
   GB_HIP(hipSetDevice(B->device));
   using namespace gbchain;

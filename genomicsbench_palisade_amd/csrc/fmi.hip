@@ -971,6 +971,7 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
 }
 
 int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
+  gb::Range range_("gb.fmi.search");
   GB_ARG(R, "gb_fmi_search: null read set");
   GB_ARG(min_seed_len > 0, "gb_fmi_search: min_seed_len %d", min_seed_len);
   GB_HIP(hipSetDevice(R->idx->device));

@@ -377,6 +377,7 @@ int gb_fmi_sa_entries(gb_fmi_index *idx, const gb_smem *smems, int64_t n, int32_
 }
 
 int gb_fmi_reads_sa_run(gb_fmi_reads *r, int32_t max_occ, int32_t mode) {
+  gb::Range range_("gb.fmi.sa_run");
   using namespace gbfmi;
   GB_ARG(r, "gb_fmi_reads_sa_run: null read set");
   GB_ARG(max_occ > 0, "gb_fmi_reads_sa_run: max_occ %d", max_occ);

@@ -272,6 +272,7 @@ struct HostTasks {
 int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *lens, const int32_t *offs, int32_t nrid,
               const HostTasks &T, int32_t min_seed_len, std::vector<std::vector<TSmem>> &recs,
               std::vector<int16_t> *next_pos, std::vector<int32_t> *rounds, int64_t *calls_out) {
+  gb::Range range_(mode == kOnePos ? "gb.fmi.onepos" : mode == kAllPos ? "gb.fmi.allpos" : "gb.fmi.last");
   const int32_t ntasks = (int32_t)T.rid.size();
   recs.assign(ntasks, {});
   if (next_pos) next_pos->assign(ntasks, 0);

@@ -1,6 +1,7 @@
 // gb_common.h -- shared host-side plumbing for the C ABI (error state, HIP checks).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -28,5 +29,13 @@ const char *last_error();
       return GB_ERR_ARG;           \
     }                              \
   } while (0)
+
+// roctx range around a host entry point (visible in rocprofv3 --marker-trace; a no-op otherwise)
+struct Range {
+  explicit Range(const char *name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range &) = delete;
+  Range &operator=(const Range &) = delete;
+};
 
 }  // namespace gb

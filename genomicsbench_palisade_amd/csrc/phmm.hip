@@ -692,6 +692,7 @@ int gb_phmm_batch_create(const gb_testcase *tcs, int n, gb_phmm_batch **out) {
 }
 
 int gb_phmm_batch_run(gb_phmm_batch *b) {
+  gb::Range range_("gb.phmm.batch_run");
   GB_ARG(b, "gb_phmm_batch_run: null batch");
   DeviceTables *t = b->tabs;
   GB_HIP(hipSetDevice(t->device));
@@ -812,6 +813,7 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
 
 int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f, double *raw_d,
                     uint8_t *used_double) {
+  gb::Range range_("gb.phmm.compute");
   GB_ARG(n >= 0 && (n == 0 || tcs), "gb_phmm_compute: bad testcase array (n=%d)", n);
   if (n == 0) return GB_OK;
   DeviceTables *tabs = nullptr;
