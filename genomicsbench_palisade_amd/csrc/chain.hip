@@ -48,6 +48,8 @@ struct Args {
   unsigned long long *visited;
   unsigned long long *prof;  // optional phase clocks (GB_CHAIN_PROF=1), see chain_kernel
   int32_t prof_call;         // the call whose consumer also records shader-clock and 100 MHz ticks
+  int32_t exp;               // PROF == 2 timing experiments (GB_CHAIN_EXP): 1 producer skips the pair
+                             // geometry, 2 consumer only drains the slots (outputs are then garbage)
 };
 
 __device__ __forceinline__ int ilog2_32(uint32_t v) { return 31 - __clz((int)v); }  // v > 0 (LogTable256)
@@ -60,11 +62,6 @@ __device__ __forceinline__ uint64_t dpp_shr_u64(uint64_t v, uint64_t lane0) {
   const int hi = dpp_shr_i32((int)(uint32_t)(v >> 32), (int)(uint32_t)(lane0 >> 32));
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
-
-// anchors are read-only for the whole kernel: the constant address space turns the uniform X[st]
-// reads of the window-start loop into scalar loads (lgkmcnt), so they never wait behind the
-// wave's outstanding score/parent/peak stores (vmcnt)
-typedef const __attribute__((address_space(4))) uint64_t const_u64;
 
 // wave-wide inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
 __device__ __forceinline__ int32_t scan_max(int32_t v) {
@@ -171,9 +168,9 @@ struct Slot {
   int32_t seq, st, q_span, pad;
 };
 
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32;
+__device__ __forceinline__ uint64_t rfl64_lane(uint64_t v, int l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32;
 }
 
 // LDS counters are read by every lane; the count is uniform, so take it into an SGPR
@@ -192,7 +189,6 @@ template <int PROF>
 __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   __shared__ uint32_t S[kRing + 64];
   __shared__ Slot ring[kSlots];
-  __shared__ uint64_t xyblk[2][2][64];  // producer's staged anchor blocks: [b & 1][x | y][k]
   __shared__ int consumed;
   const int c = A.order[blockIdx.x];
   const int lane = threadIdx.x & 63;
@@ -203,7 +199,6 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
   const double avg_qspan = (double)A.avg_qspan[c];
   const uint64_t *X = A.x + o, *Y = A.y + o;
-  const const_u64 *XC = (const const_u64 *)X;
   int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
 
   for (int k = threadIdx.x; k < kRing + 64; k += 128) S[k] = 0;
@@ -219,29 +214,50 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     int32_t st = 0;
     const bool pc = PROF == 2 && c == A.prof_call;
     unsigned long long p_load = 0, p_wait = 0, t0 = 0;
-    // Anchors x/y reach the producer through LDS, a 64-anchor block ahead: at the start of block
-    // b the block loaded at the start of b-1 (one coalesced load per array; its only wait is here)
-    // goes into xy[b & 1], and block b+1 is requested. No load sits on the per-anchor path, which
-    // keeps the producer ahead when L2/HBM are busy with other calls. The window start's x is kept
-    // in SGPRs and refreshed by a scalar load only when st advances.
-    uint64_t nx = X[min(lane, n - 1)], ny = Y[min(lane, n - 1)];
-    uint64_t xst = n > 0 ? XC[0] : 0;
+    // Anchor blocks: bx/by hold X/Y[64b .. 64b+63] (lane k = anchor 64b+k) and the next block is
+    // loaded one block ahead, so x[i], y[i] are register reads (readlane), not LDS round trips.
+    uint64_t bx = X[min(lane, n - 1)], by = Y[min(lane, n - 1)];
+    uint64_t nx = X[min(64 + lane, n - 1)], ny = Y[min(64 + lane, n - 1)];
+    // The window start st: X[sb .. sb+63] (sb = st rounded down to 64) sits in a VGPR, the next
+    // block is loaded one block ahead, and st advances by one ballot over the block instead of a
+    // chain of dependent scalar loads (while (st < i && x[i] > x[st] + max_dist_x) ++st).
+    int32_t sb = 0;
+    uint64_t sx = bx, sxn = nx;
+    const uint64_t mdx = (uint64_t)(int64_t)max_dist_x;
+    // the consumer's progress, read one anchor ahead (a stale value only delays; it never lets the
+    // producer overwrite an unread slot)
+    int32_t cons_v = 0;
     for (int32_t iv = 0; iv < n; iv++) {
       // opaque to loop strength reduction, which otherwise derives i from the per-lane i-1-lane
       // (a VGPR induction variable) and turns every uniform value below into a vector one
       const int32_t i = __builtin_amdgcn_readfirstlane(iv);
       if (pc) t0 = __builtin_amdgcn_s_memtime();
-      if ((i & 63) == 0) {
-        xyblk[(i >> 6) & 1][0][lane] = nx;
-        xyblk[(i >> 6) & 1][1][lane] = ny;
+      if ((i & 63) == 0 && i > 0) {
+        bx = nx;
+        by = ny;
         nx = X[min(i + 64 + lane, n - 1)];
         ny = Y[min(i + 64 + lane, n - 1)];
       }
-      const uint64_t xi = rfl64(xyblk[(i >> 6) & 1][0][i & 63]), yi = rfl64(xyblk[(i >> 6) & 1][1][i & 63]);
-      while (st < i && xi > xst + (uint64_t)(int64_t)max_dist_x) xst = XC[++st];
+      const uint64_t xi = rfl64_lane(bx, i & 63), yi = rfl64_lane(by, i & 63);
+      while (true) {  // first j >= st that stops the scan (j == i, or x[i] <= x[j] + max_dist_x)
+        const int32_t jl = sb + lane;
+        const uint64_t stop = __builtin_amdgcn_ballot_w64((jl >= st) & ((jl >= i) | !(xi > sx + mdx)));
+        if (stop) {
+          st = sb + __builtin_ctzll(stop);
+          break;
+        }
+        sb += 64;  // every candidate of the block passed: next block
+        sx = sxn;
+        sxn = X[min(sb + 64 + lane, n - 1)];
+        st = sb;
+      }
       if (i - st > kMaxIter) {  // rare: > max_iter candidates in range
         st = i - kMaxIter;
-        xst = XC[st];
+        if (st >= sb + 64) {
+          sb = st & ~63;
+          sx = X[min(sb + lane, n - 1)];
+          sxn = X[min(sb + 64 + lane, n - 1)];
+        }
       }
       if (pc) {
         __builtin_amdgcn_s_waitcnt(0);
@@ -249,102 +265,194 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
         p_load += t1 - t0;
       }
       int32_t sg;
-      const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+      bool ok;
+      if (PROF >= 1 && (A.exp & 1)) {
+        ok = i - 1 - lane >= st;
+        sg = 1;
+      } else {
+        ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+      }
       // wait for a free slot
       if (pc) t0 = __builtin_amdgcn_s_memtime();
-      while (i - lds_count(&consumed) >= kSlots) __builtin_amdgcn_s_sleep(1);
+      if (i - __builtin_amdgcn_readfirstlane(cons_v) >= kSlots)
+        while (i - lds_count(&consumed) >= kSlots) __builtin_amdgcn_s_sleep(1);
       if (pc) p_wait += __builtin_amdgcn_s_memtime() - t0;
       Slot &sl = ring[i & (kSlots - 1)];
       sl.sg[lane] = ok ? sg : kNoCand;
       if (lane == 0) {
         sl.st = st;
         sl.q_span = (int32_t)(yi >> 32 & 0xff);
+        // published after the contents: the LDS performs one wave's accesses in issue order
+        __hip_atomic_store(&sl.seq, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // slot contents land before the seq that publishes them
-      if (lane == 0) __hip_atomic_store(&sl.seq, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      cons_v = __hip_atomic_load(&consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       wx = dpp_shr_u64(wx, xi);
       wy = dpp_shr_u64(wy, yi);
     }
+    {  // slot n: no candidates (the consumer precomputes one anchor ahead and reads it last)
+      while (n - lds_count(&consumed) >= kSlots) __builtin_amdgcn_s_sleep(1);
+      Slot &sl = ring[n & (kSlots - 1)];
+      sl.sg[lane] = kNoCand;
+      if (lane == 0) {
+        sl.st = n;
+        sl.q_span = 0;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (lane == 0) __hip_atomic_store(&sl.seq, n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (pc && lane == 0) {
-      atomicAdd(A.prof + 12, p_load);
-      atomicAdd(A.prof + 13, p_wait);
+      atomicAdd(A.prof + 14, p_load);
+      atomicAdd(A.prof + 15, p_wait);
     }
     return;
   }
 
   // ---------------- consumer ---------------------------------------------------------------------
-  const bool pc = PROF == 2 && c == A.prof_call;  // phase clocks for the profiled call only
+  // Anchor i's first 64 candidates (lane l = j = i-1-l) are resolved in two parts. Everything that
+  // does not depend on anchor i-1's own result is prepared one iteration early, while anchor i-1 is
+  // still open: the partial scores of lanes >= 1 (their scores are known), their exclusive running
+  // maximum, and the LDS stamps of the parents of lanes >= 1 (read back in the next iteration, so
+  // the LDS latency is hidden). Once f[i-1] and p[i-1] arrive, what is left is lane 0's score (a
+  // scalar add), one max + compare per lane for the improvements, lane 0's mark (one bit), and the
+  // n_skip walk, which runs in scalar registers over the improvement and target bitmasks.
   const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(target, (short)0, n * 4, 0x00020000);
   const int32_t neg_lane = -lane;
-  int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l
-  unsigned long long vis = 0;
-  unsigned long long c_head = 0, c_step = 0, c_tail = 0, n_step = 0, n_miss = 0, c_miss = 0, t_0 = 0, t_1 = 0;
-  // slot i is read during step i-1 (header first: LDS executes a wave's reads in order, so a
-  // matching seq means the sg read after it saw the complete slot)
-  // volatile LDS (address space 3) reads: kept in program order (seq before sg) and still ds_read
+  int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l (top of iteration i)
+  unsigned long long vis = 0, n_mem = 0, n_miss = 0, c_pre = 0, c_crit = 0, c_tail = 0, n_walk = 0, c_um = 0, c_walk = 0;
   typedef int32_t v4i __attribute__((ext_vector_type(4)));
   typedef volatile __attribute__((address_space(3))) v4i lds_v4i;
   typedef volatile __attribute__((address_space(3))) int32_t lds_i32;
+  // slot a is read ahead (header first: LDS executes a wave's reads in order, so a matching seq
+  // means the sg read after it saw the complete slot); slot n is the producer's empty sentinel
   v4i hdr = *(lds_v4i *)&ring[0].seq;
   int32_t psg = *(lds_i32 *)&ring[0].sg[lane];
-  unsigned long long clk0 = 0, rt0 = 0;
+  auto take = [&](int32_t a, int32_t &st, int32_t &q_span, int32_t &sg) {
+    if (__builtin_amdgcn_readfirstlane(hdr.x) == a + 1) {
+      st = __builtin_amdgcn_readfirstlane(hdr.y);
+      q_span = __builtin_amdgcn_readfirstlane(hdr.z);
+      sg = psg;
+    } else {  // the producer was behind when the slot was read ahead: wait for it, read again
+      if (PROF) ++n_miss;
+      Slot &sl = ring[a & (kSlots - 1)];
+      while (lds_count(&sl.seq) != a + 1) __builtin_amdgcn_s_sleep(1);
+      st = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.st);
+      q_span = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.q_span);
+      sg = *(lds_i32 *)&sl.sg[lane];
+    }
+    // free slot a (its reads were issued before this write, and LDS runs them in order), then
+    // read slot a+1 ahead
+    if (lane == 0) __hip_atomic_store(&consumed, a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    Slot &nl = ring[(a + 1) & (kSlots - 1)];
+    hdr = *(lds_v4i *)&nl.seq;
+    psg = *(lds_i32 *)&nl.sg[lane];
+  };
+  // prepared state of the anchor about to be resolved (the names of anchor a, lanes >= 1):
+  //   psc  sg + score[j] (INT_MIN when filtered)   pB  max(q_span, psc of lanes 1..l-1)
+  //   ppj  parent[j]                               pt  stamp read back at j (targeted iff == a+1)
+  int32_t psc, pB, ppj, pt, pok, pst, pq, psg0;
+  auto prepare_math = [&](int32_t a, int32_t sg, int32_t ws1, int32_t wp1) {
+    const bool ok = sg != kNoCand;
+    pok = ok;
+    psc = ok ? (int32_t)((uint32_t)sg + (uint32_t)ws1) : INT_MIN;
+    if (PROF >= 1 && (A.exp & 4)) {
+      pB = pq;
+    } else {
+      const int32_t mx = scan_max(lane == 0 ? INT_MIN : psc);
+      pB = max(dpp_shr_i32(mx, INT_MIN), pq);
+    }
+    ppj = wp1;
+    // "targets[j] == a" from the parents of lanes >= 1: a stamp a+1 at each parent (a parent is an
+    // earlier anchor, so only later lanes can be hit); read back here, consumed one iteration later
+    if (PROF >= 1 && (A.exp & 8)) {
+      pt = 0;
+    } else {
+      S[(ok & (lane > 0) & (wp1 >= pst)) ? (wp1 & (kRing - 1)) : kRing + lane] = (uint32_t)(a + 1);
+      pt = (int32_t)S[(a - 1 - lane) & (kRing - 1)];
+    }
+    psg0 = __builtin_amdgcn_readfirstlane(sg);
+  };
+  unsigned long long rt0 = 0, clk0 = 0;
   if (PROF) {
-    clk0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
+    clk0 = __builtin_amdgcn_s_memtime();
   }
+  const bool pc = PROF == 2 && c == A.prof_call;
+  {
+    int32_t sg;
+    take(0, pst, pq, sg);
+    prepare_math(0, sg, 0, -1);
+  }
+  int32_t Mprev = 0, Jprev = -1;
   for (int32_t base = 0; base < n; base += 64) {
     const int32_t cnt = min(64, n - base);
     for (int32_t k = 0; k < cnt; k++) {
       const int32_t i = __builtin_amdgcn_readfirstlane(base + k);
-      if (pc) t_0 = __builtin_amdgcn_s_memtime();
-      int32_t st, q_span, sg;
-      if (__builtin_amdgcn_readfirstlane(hdr.x) == i + 1) {
-        st = __builtin_amdgcn_readfirstlane(hdr.y);
-        q_span = __builtin_amdgcn_readfirstlane(hdr.z);
-        sg = psg;
-      } else {  // the producer was behind when the slot was read ahead: wait for it, read again
-        if (pc) {
-          ++n_miss;
-          t_1 = __builtin_amdgcn_s_memtime();
-        }
-        Slot &sl = ring[i & (kSlots - 1)];
-        while (lds_count(&sl.seq) != i + 1) __builtin_amdgcn_s_sleep(1);
-        if (pc) c_miss += __builtin_amdgcn_s_memtime() - t_1;
-        st = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.st);
-        q_span = __builtin_amdgcn_readfirstlane(*(lds_i32 *)&sl.q_span);
-        sg = *(lds_i32 *)&sl.sg[lane];
+      if (PROF >= 1 && (A.exp & 2)) {
+        int32_t a0, a1, a2;
+        take(i + 1, a0, a1, a2);
+        continue;
       }
-      // free slot i (its reads were issued before this write, and LDS runs them in order), then
-      // read slot i+1 ahead; its latency overlaps this step
-      if (lane == 0) __hip_atomic_store(&consumed, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      {
-        Slot &nl = ring[(i + 1) & (kSlots - 1)];
-        hdr = *(lds_v4i *)&nl.seq;
-        psg = *(lds_i32 *)&nl.sg[lane];
-      }
-      const bool ok = sg != kNoCand;
-      int32_t M = q_span, N = 0, J = -1;
-      const uint32_t stamp = (uint32_t)(i + 1);
-      uint32_t vis_i = 0;
-      if (pc) {
-        t_1 = __builtin_amdgcn_s_memtime();
-        c_head += t_1 - t_0;
-        t_0 = t_1;
-      }
+      unsigned long long t0 = 0;
+      if (pc) t0 = __builtin_amdgcn_s_memtime();
+      // this anchor's prepared state
+      const int32_t sc = psc, B = pB, pjv_hi = ppj, st = __builtin_amdgcn_readfirstlane(pst),
+                    q_span = __builtin_amdgcn_readfirstlane(pq), sg0 = psg0;
+      const uint64_t okm = __builtin_amdgcn_ballot_w64(pok != 0);
+      const uint64_t tgtm = __builtin_amdgcn_ballot_w64(pt == i + 1) & ~1ull;
+      // the next anchor's slot (the only branch before the resolve: a producer that fell behind)
+      int32_t sgn;
+      take(i + 1, pst, pq, sgn);
+      // From here to the walk's result the code is one basic block: the next anchor's preparation
+      // (independent of this anchor's result) and this anchor's resolution interleave.
+      const int32_t ws1 = dpp_shr_i32(ws, 0), wp1 = dpp_shr_i32(wpar, -1);
+      prepare_math(i + 1, sgn, ws1, wp1);
+      // ---- anchor i: no candidate passes the filters when jtop < st (okm == 0) ----------------
       const int32_t jtop = i - 1;
-      bool brk = false;
-      if (jtop >= st) {
-        if (pc) ++n_step;
-        const int32_t sc = ok ? (int32_t)((uint32_t)sg + (uint32_t)ws) : INT_MIN;
-        brk = resolve_step(sc, ok, wpar, jtop, st, stamp, lane, neg_lane, trs, i, S, M, J, N, vis_i);
-      }
-      if (!brk && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
-        // the wave's flushed score/parent stores reach L2 before these sc1 reads of them (the
-        // drain sits here, not at every flush, so the common path never waits on a store)
+      const bool ok0 = okm & 1;
+      const int32_t sc0 = ok0 ? (int32_t)((uint32_t)sg0 + (uint32_t)Mprev) : INT_MIN;
+      // improvements: lane 0 against q_span, lanes >= 1 against max(q_span, sc0, earlier lanes)
+      const uint64_t um = (__builtin_amdgcn_ballot_w64(sc > max(B, sc0)) & ~1ull) | (uint64_t)(sc0 > q_span);
+      const int32_t dl = jtop - Jprev;  // lane 0 marks p[i-1]
+      const uint64_t tg = tgtm | ((ok0 & (Jprev >= 0) & (dl < 64)) ? (1ull << (dl & 63)) : 0ull);
+      // n_skip walk (host_kernel.cpp:81-88) over the lanes in visiting order: n after lane l is the
+      // reflected walk max(D_l, D_l - min_{k<=l} D_k) of D_l = targeted non-improving minus
+      // improving lanes up to l (n starts at 0; lane 0 is never targeted); the break is the first
+      // targeted non-improving lane where n exceeds max_skip
+      const uint64_t pm = okm & ~um & tg;
+      const bool plus = (pm >> lane) & 1, upd = (um >> lane) & 1;
+      const uint64_t num = ~um;
+      const int32_t d_ex = (int32_t)__builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(num >> 32),
+          __builtin_amdgcn_mbcnt_lo((uint32_t)num, __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)pm, (uint32_t)neg_lane))));
+      const int32_t D = d_ex + (plus ? 1 : (upd ? -1 : 0));
+      const int32_t n_after = max(D, D - scan_min(D));
+      const uint64_t bm = __builtin_amdgcn_ballot_w64(plus & (n_after > kMaxSkip));
+      const int32_t b = bm ? __builtin_ctzll(bm) : 64;
+      const uint64_t below = bm ? (bm - 1) & ~bm : ~0ull;
+      const int32_t nvalid = max(0, min(64, jtop - st + 1));
+      uint32_t vis_i = bm ? (uint32_t)b + 1 : (uint32_t)nvalid;
+      const uint64_t ume = um & below;
+      const int32_t lu = 63 - __builtin_clzll(ume | 1);
+      const int32_t m_lu = __builtin_amdgcn_readlane(sc, lu);
+      int32_t M = ume ? (lu == 0 ? sc0 : m_lu) : q_span;
+      int32_t J = ume ? jtop - lu : -1;
+      // targets[p[j]] = i for the visited lanes that passed the filters
+      const int32_t pjv = lane == 0 ? Jprev : pjv_hi;
+      const bool wt = (bool)((okm & below) >> lane & 1) & (pjv >= 0);
+      if (!(PROF >= 1 && (A.exp & 32)))
+        __builtin_amdgcn_raw_buffer_store_b32(i, trs, wt ? (uint32_t)pjv * 4u : 0xFFFFFFFFu, 0, 0);
+      if (!bm && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
+        if (PROF) ++n_mem;
+        // this anchor's own stamps first (the next anchor's preparation overwrote them)
+        const uint32_t stamp = (uint32_t)(i + 1);
+        const bool okl = (okm >> lane) & 1;
+        S[(okl & (pjv >= st)) ? (pjv & (kRing - 1)) : kRing + lane] = stamp;
+        // the wave's flushed score/parent stores reach L2 before these sc1 reads of them
         __builtin_amdgcn_s_waitcnt(0);
         const uint64_t xi = X[i], yi = Y[i];
+        int32_t N = __builtin_amdgcn_readlane(n_after, 63);
         for (int32_t jt = jtop - 64; jt >= st; jt -= 64) {
-          if (pc) ++n_step;
           const int32_t jj = jt - lane;
           const bool v = jj >= st;
           uint64_t xj = 0, yj = 0;
@@ -363,20 +471,22 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
         }
       }
       vis += vis_i;
+      unsigned long long t2 = 0;
       if (pc) {
-        t_1 = __builtin_amdgcn_s_memtime();
-        c_step += t_1 - t_0;
-        t_0 = t_1;
+        t2 = __builtin_amdgcn_s_memtime();
+        c_crit += t2 - t0;
       }
       // peak of the parent: from the register window when J >= i-64, else (rare) from memory
       const int32_t dJ = i - 1 - J;
       int32_t pkJ = __builtin_amdgcn_readlane(wpk, dJ & 63);
       if (J >= 0 && dJ > 63) pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
-      const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
-      ws = dpp_shr_i32(ws, M);
-      wpar = dpp_shr_i32(wpar, J);
+      const int32_t pki = (PROF >= 1 && (A.exp & 64)) ? M : (J >= 0 && pkJ > M) ? pkJ : M;
+      ws = lane == 0 ? M : ws1;
+      wpar = lane == 0 ? J : wp1;
       wpk = dpp_shr_i32(wpk, pki);
-      if (pc) c_tail += __builtin_amdgcn_s_memtime() - t_0;
+      Mprev = M;
+      Jprev = J;
+      if (pc) c_tail += __builtin_amdgcn_s_memtime() - t2;
     }
     // flush the window: anchors base .. base+cnt-1 (lane l: base+cnt-1-l)
     if (lane < cnt) {
@@ -392,16 +502,14 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     if (c == A.prof_call) {
       atomicAdd(A.prof + 9, rt0);
       atomicAdd(A.prof + 10, rt1);
-    }
-  }
-  if (pc && lane == 0) {
-    atomicAdd(A.prof + 0, c_head);
-    atomicAdd(A.prof + 1, c_step);
-    atomicAdd(A.prof + 2, c_tail);
-    atomicAdd(A.prof + 3, n_step);
-    atomicAdd(A.prof + 4, n_miss);
-    atomicAdd(A.prof + 5, c_miss);
-    if (c == A.prof_call) {
+      atomicAdd(A.prof + 0, c_pre);
+      atomicAdd(A.prof + 1, c_crit);
+      atomicAdd(A.prof + 2, c_tail);
+      atomicAdd(A.prof + 3, n_mem);
+      atomicAdd(A.prof + 4, n_miss);
+      atomicAdd(A.prof + 5, n_walk);
+      atomicAdd(A.prof + 12, c_um);
+      atomicAdd(A.prof + 13, c_walk);
       atomicAdd(A.prof + 6, __builtin_amdgcn_s_memtime() - clk0);
       atomicAdd(A.prof + 7, __builtin_amdgcn_s_memrealtime() - rt0);
     }
@@ -539,11 +647,12 @@ int gb_chain_batch_run(gb_chain_batch *B) {
     A.visited = B->d_vis;
     A.prof = nullptr;
     A.prof_call = -1;
+    A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
     const char *pe = getenv("GB_CHAIN_PROF");
     const int prof = (pe && (*pe == '1' || *pe == '2')) ? *pe - '0' : 0;
     if (prof) {
-      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 14 * sizeof(unsigned long long)));
-      GB_HIP(hipMemsetAsync(B->d_prof, 0, 14 * sizeof(unsigned long long), B->stream));
+      if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 16 * sizeof(unsigned long long)));
+      GB_HIP(hipMemsetAsync(B->d_prof, 0, 16 * sizeof(unsigned long long), B->stream));
       GB_HIP(hipMemsetAsync(B->d_prof + 8, 0xff, sizeof(unsigned long long), B->stream));
       A.prof = B->d_prof;
       int32_t c0 = 0;
@@ -560,14 +669,15 @@ int gb_chain_batch_run(gb_chain_batch *B) {
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   if (B->d_prof && getenv("GB_CHAIN_PROF")) {
-    unsigned long long h[14];
+    unsigned long long h[16];
     GB_HIP(hipMemcpyAsync(h, B->d_prof, sizeof(h), hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
-    fprintf(stderr, "[chain prof] memtime ticks: head %llu steps %llu tail %llu; steps %llu; slot misses %llu (%llu ticks); "
-            "longest call %llu clk / %llu rt ticks = %.0f MHz\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7],
-            h[7] ? 100.0 * (double)h[6] / (double)h[7] : 0.0);
-    fprintf(stderr, "[chain prof] grid %.3f ms; longest call starts at %.3f ms, ends at %.3f ms; producer load %llu wait %llu\n",
-            (double)(h[11] - h[8]) * 1e-5, (double)(h[9] - h[8]) * 1e-5, (double)(h[10] - h[8]) * 1e-5, h[12], h[13]);
+    fprintf(stderr, "[chain prof] longest call, memtime ticks: prepare %llu resolve %llu tail %llu; memory passes %llu; "
+            "slot misses %llu; walk iterations %llu; total %llu clk / %llu rt ticks = %.0f MHz\n", h[0], h[1], h[2], h[3],
+            h[4], h[5], h[6], h[7], h[7] ? 100.0 * (double)h[6] / (double)h[7] : 0.0);
+    fprintf(stderr, "[chain prof] grid %.3f ms; longest call starts at %.3f ms, ends at %.3f ms; producer load %llu wait %llu; "
+            "resolve: to um %llu, walk %llu\n", (double)(h[11] - h[8]) * 1e-5, (double)(h[9] - h[8]) * 1e-5,
+            (double)(h[10] - h[8]) * 1e-5, h[14], h[15], h[12], h[13]);
   }
   B->ran = true;
   return GB_OK;
