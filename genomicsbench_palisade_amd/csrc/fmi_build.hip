@@ -292,17 +292,22 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
   // (3) BWT -> CP_OCC (counts = exclusive scan of per-block base counts), sentinel row
   const int64_t n = N + 1;
   const int64_t nblocks = (n >> 6) + 1;
-  auto *idx = new gb_fmi_index();
+  // every return below (error or not) goes through the guard: an unfinished index is destroyed
+  struct IdxGuard {
+    gb_fmi_index *p;
+    ~IdxGuard() {
+      if (p) gb_fmi_index_destroy(p);
+    }
+  } guard{new gb_fmi_index()};
+  gb_fmi_index *const idx = guard.p;
   GB_HIPX(hipGetDevice(&idx->device));
   hipError_t e = hipMalloc(&idx->d_occ, sizeof(CpOcc) * (size_t)nblocks);
   if (e != hipSuccess) {
-    delete idx;
     gb::set_error("gb_fmi_index_build: %s", hipGetErrorString(e));
     return GB_ERR_HIP;
   }
   DevBuf d_cnt, d_scan;
   if ((st = dalloc<int64_t>(d_cnt, 4 * nblocks)) || (st = dalloc<int64_t>(d_scan, 4 * nblocks))) {
-    gb_fmi_index_destroy(idx);
     return st;
   }
   hipLaunchKernelGGL(occ_blocks, dim3(grid(nblocks)), dim3(256), 0, s, d_text.as<uint8_t>(), sa, N, nblocks,
@@ -311,7 +316,6 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
   GB_HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, tb64, d_cnt.as<int64_t>(), d_scan.as<int64_t>(), (int)nblocks, s));
   DevBuf d_tmp64;
   if ((st = dalloc<uint8_t>(d_tmp64, (int64_t)tb64 + 16))) {
-    gb_fmi_index_destroy(idx);
     return st;
   }
   for (int q = 0; q < 4; q++) {
@@ -348,7 +352,6 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
   const int64_t ns = (n >> 3) + 1;
   idx->sa_ns = ns;
   if (hipMalloc(&idx->d_sa, sizeof(int64_t) * (size_t)ns) != hipSuccess) {
-    gb_fmi_index_destroy(idx);
     gb::set_error("gb_fmi_index_build: out of device memory (sampled SA)");
     return GB_ERR_HIP;
   }
@@ -360,8 +363,7 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
   } else {
     DevBuf d_ms, d_ls;
     if ((st = dalloc<int8_t>(d_ms, ns)) || (st = dalloc<uint32_t>(d_ls, ns))) {
-      gb_fmi_index_destroy(idx);
-      return st;
+        return st;
     }
     hipLaunchKernelGGL(sample_sa, dim3(grid(ns)), dim3(256), 0, s, sa, N, ns, d_ms.as<int8_t>(), d_ls.as<uint32_t>(),
                        idx->d_sa);
@@ -373,8 +375,7 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
     GB_HIPX(hipMemcpy(ls.data(), d_ls.p, 4 * (size_t)ns, hipMemcpyDeviceToHost));
     FILE *fp = fopen(out_path, "wb");
     if (!fp) {
-      gb_fmi_index_destroy(idx);
-      gb::set_error("gb_fmi_index_build: cannot write %s", out_path);
+        gb::set_error("gb_fmi_index_build: cannot write %s", out_path);
       return GB_ERR_ARG;
     }
     fwrite(&n, 8, 1, fp);
@@ -386,5 +387,6 @@ extern "C" int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, con
     fclose(fp);
   }
   *out = idx;
+  guard.p = nullptr;  // handed to the caller
   return GB_OK;
 }
