@@ -362,7 +362,17 @@ def phmm_dropin_e2e(args, D, ta, cells, rank, world):
     lib = ctypes.CDLL(os.path.join(ROOT, "genomicsbench_palisade_amd", "lib", "libgkl_pairhmm_c.so"))
     both = getattr(lib, "_Z22computelikelihoodsbothP8testcasePdi")
     both.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-    getattr(lib, "_Z11initPairHMMv")()
+    # initPairHMM prints a banner on stdout like the reference's (IntelPairHmmCSource.cpp:34); the
+    # bench's stdout carries only its JSON line, so the banner goes to stderr
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        getattr(lib, "_Z11initPairHMMv")()
+        ctypes.CDLL(None).fflush(None)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     out = np.zeros(max(ta.n, 1))
     D.barrier()
     t = D.max(e2e_time(lambda: both(ctypes.addressof(ta.arr), out.ctypes.data, ta.n)))
@@ -698,7 +708,7 @@ def bench_fmi(args, D, rank, world):
                                          "counts D2H (index already resident)"}}
     sa = bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens)
     rs.close()
-    small = bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref)
+    small = None if args.no_small else bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref)
     idx.close()
     return {
         "value": round(mreads, 3), "unit": "Mreads/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),

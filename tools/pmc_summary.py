@@ -1,5 +1,4 @@
-"""Summarise rocprofv3 runs of bench.py into profiles/<tag>_pmc.json: per hot kernel (fmi pass 1 and
-pass 2 told apart by grid size) the mean duration and the HBM bytes per launch from FETCH_SIZE and
+"""Summarise rocprofv3 runs of bench.py into profiles/<tag>_pmc.json: per hot kernel the mean duration and the HBM bytes per launch from FETCH_SIZE and
 WRITE_SIZE (separate passes), KiB x 1024.
 
 Correction, as MI355X_MICROARCH.md's HBM section prescribes ("calibrate on a known byte count in
@@ -44,7 +43,10 @@ def name_of(r):
 
 def load(d):
     """Per kernel name: one (bytes, ms) entry per dispatch; the variants of a multi-launch step
-    (bsw_lane_kernel<NCH>) are merged per step by summing consecutive dispatches of one step."""
+    (bsw_lane_kernel<NCH>) are merged per step by summing consecutive dispatches of one step.
+    Launches of one kernel over different workloads (e.g. a second, smaller leg) would be averaged
+    together, so the profiling passes run the large legs only and main() refuses a kernel whose
+    launches differ in size by more than 10 %."""
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         n = name_of(r)
@@ -71,6 +73,9 @@ def main():
         fb = [v for v, _ in f.get(k, [])]
         wb = [v for v, _ in w.get(k, [])]
         ms = [d for _, d in f.get(k, [])] + [d for _, d in w.get(k, [])]
+        for vals in (fb, wb):
+            if vals and max(vals) > 1.1 * min(vals):
+                sys.exit(f"{k}: launches of different sizes ({min(vals):.3g} .. {max(vals):.3g} B); profile one leg")
         raw = sum(fb) / max(len(fb), 1)
         cls = KERNEL_CLASS.get(k, "gather")
         res[k] = {"launches": len(fb), "fetch_bytes": raw * FETCH_FACTOR[cls], "fetch_bytes_raw": raw,
