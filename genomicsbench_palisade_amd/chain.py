@@ -19,6 +19,7 @@ def _decl():
     L.gb_chain_batch_sync.argtypes = [vp]
     L.gb_chain_batch_results.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gb_chain_batch_timing.argtypes = [vp, vp]
+    L.gb_chain_batch_split_stats.argtypes = [vp, vp, vp, vp]
     L.gb_chain_batch_destroy.argtypes = [vp]
     L.gb_chain_batch_backtrack.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
     L.gb_chain_batch_chains.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
@@ -54,6 +55,12 @@ class ChainBatch:
         ms = ctypes.c_float()
         check(_decl().gb_chain_batch_timing(self.h, ctypes.byref(ms)), "gb_chain_batch_timing")
         return ms.value
+
+    def split_stats(self):
+        """-> (calls run as speculative segments, guess/verify rounds, fix-up blocks) of the last run."""
+        v = [ctypes.c_int64() for _ in range(3)]
+        check(_decl().gb_chain_batch_split_stats(self.h, *[ctypes.byref(x) for x in v]), "gb_chain_batch_split_stats")
+        return tuple(x.value for x in v)
 
     def backtrack(self, min_cnt: int = 3, min_sc: int = 40):
         """minimap2's chain backtrack on this batch's chain_dp outputs (asynchronous)."""

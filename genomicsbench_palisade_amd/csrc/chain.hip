@@ -31,134 +31,22 @@
 #include "../../include/gb_chain.h"
 #include "gb_common.h"
 #include "chain_internal.h"
+#include "chain_dev.h"
 
 namespace gbchain {
 
-constexpr int kRing = 8192;     // stamp ring >= max_iter (5000) + 64 candidates
-constexpr int kMaxIter = 5000;  // host_kernel.cpp:41
-constexpr int kMaxSkip = 25;    // host_kernel.cpp:42
-
 struct Args {
-  const int64_t *offsets;
+  const VCall *vc;  // blocks, longest first
   const float *avg_qspan;
   const int32_t *params4;
   const uint64_t *x, *y;
-  const int32_t *order;  // calls, longest first
   int32_t *score, *parent, *target, *peak;
+  int32_t *s_score, *s_parent;  // segment scratch (kVScratch blocks)
   unsigned long long *visited;
   unsigned long long *prof;  // optional phase clocks (GB_CHAIN_PROF=1), see chain_kernel
-  int32_t prof_call;         // the call whose consumer also records shader-clock and 100 MHz ticks
   int32_t exp;               // PROF == 2 timing experiments (GB_CHAIN_EXP): 1 producer skips the pair
                              // geometry, 2 consumer only drains the slots (outputs are then garbage)
 };
-
-__device__ __forceinline__ int ilog2_32(uint32_t v) { return 31 - __clz((int)v); }  // v > 0 (LogTable256)
-
-__device__ __forceinline__ int dpp_shr_i32(int v, int lane0) {
-  return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
-}
-__device__ __forceinline__ uint64_t dpp_shr_u64(uint64_t v, uint64_t lane0) {
-  const int lo = dpp_shr_i32((int)(uint32_t)v, (int)(uint32_t)lane0);
-  const int hi = dpp_shr_i32((int)(uint32_t)(v >> 32), (int)(uint32_t)(lane0 >> 32));
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
-
-// wave-wide inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
-__device__ __forceinline__ int32_t scan_max(int32_t v) {
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xF, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xA, 0xF, false));
-  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xC, 0xF, false));
-  return v;
-}
-__device__ __forceinline__ int32_t scan_min(int32_t v) {
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xF, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xA, 0xF, false));
-  v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xC, 0xF, false));
-  return v;
-}
-__device__ __forceinline__ int32_t load_l2(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1 (bypasses L1)
-}
-
-// Pair geometry of anchor i against candidate j (host_kernel.cpp:55-82 without score[j]): whether j
-// passes the filters, and s = min(q_span, dq, dr) (+1 paired bonus) - gap_cost.
-__device__ __forceinline__ bool geometry(uint64_t xi, uint64_t yi, uint64_t xj, uint64_t yj, bool valid,
-                                         int max_dist_x, int max_dist_y, int bw, int n_segs, double avg_qspan,
-                                         int32_t &sg) {
-  const int32_t qi = (int32_t)yi, q_span = (int32_t)(yi >> 32 & 0xff);
-  const int32_t sidi = (int32_t)((yi & (0xffull << 48)) >> 48);
-  const int64_t dr = (int64_t)(xi - xj);
-  const int32_t dq = qi - (int32_t)yj;
-  const int32_t sidj = (int32_t)((yj & (0xffull << 48)) >> 48);
-  const bool same = sidi == sidj;
-  const int32_t dd = (int32_t)(dr > dq ? dr - dq : dq - dr);
-  // bitwise predicates and selects throughout: per-lane branches would cost exec-mask regions
-  const bool ok = valid & !((same & (dr == 0)) | (dq <= 0)) & !((same & (dq > max_dist_y)) | (dq > max_dist_x)) &
-                  !(same & (dd > bw)) & !((n_segs > 1) & same & (dr > max_dist_y));  // is_cdna = 0
-  const int32_t min_d = (int32_t)(dq < dr ? (int64_t)dq : dr);
-  const int log_dd = dd ? ilog2_32((uint32_t)dd) : 0;
-  const int c_lin = (int)((double)dd * .01 * avg_qspan);
-  const int32_t s0 = min_d > q_span ? q_span : min_d;
-  // different sequences: +1 on dr == 0 and gap min(c_lin, log_dd) unless dr == 0; same: c_lin + log_dd/2
-  const int32_t gap_diff = dr == 0 ? 0 : (c_lin < log_dd ? c_lin : log_dd);
-  const int32_t gap_same = c_lin + (log_dd >> 1);
-  const int32_t bonus = (!same & (dr == 0)) ? 1 : 0;
-  // (int)((double)gap_cost * gap_scale + .499) with gap_scale == 1.0f (host_kernel.cpp:36) is
-  // gap_cost itself for 0 <= gap_cost < 2^31
-  sg = s0 + bonus - (same ? gap_same : gap_diff);
-  return ok;
-}
-
-constexpr int32_t kNoCand = INT_MIN;  // sg of a filtered candidate (producer -> consumer)
-
-// One 64-candidate step in visiting order (lane l = j = jtop - l): running max_f, n_skip, the
-// break and the targets/stamps. sc is INT_MIN on filtered lanes (ok false). Updates M, J, N;
-// returns whether the step broke. Indices are int32 (calls hold < 2^30 anchors, checked at batch
-// creation) so uniform compares stay on the SALU, and the step has no exec-mask branch: lanes with
-// nothing to mark stamp a private dummy word S[kRing + lane], and the targets store is a buffer
-// store whose disabled lanes carry an out-of-range offset.
-__device__ __forceinline__ bool resolve_step(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, uint32_t stamp,
-                                             int lane, int32_t neg_lane, __amdgpu_buffer_rsrc_t trs, int32_t i,
-                                             uint32_t *S, int32_t &M, int32_t &J, int32_t &N, uint32_t &vis) {
-  // "targets[j] == i": stamps from visited j' > j with parents[j'] == j. A stamp can only match a
-  // lane whose j >= st (|pj - j| < kRing, so equal ring slots mean pj == j), so no validity test
-  S[(ok & (pj >= st)) ? (pj & (kRing - 1)) : kRing + lane] = stamp;
-  const bool tgt = S[(jtop - lane) & (kRing - 1)] == stamp;
-  const int32_t mx = scan_max(sc);  // inclusive max scan
-  const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
-  const bool upd = sc > before;  // false on filtered lanes: before >= M >= 0 > INT_MIN
-  const bool plus = ok & !upd & tgt;
-  const uint64_t um_all = __builtin_amdgcn_ballot_w64(upd), pm = __builtin_amdgcn_ballot_w64(plus);
-  // n_skip after lane l as a reflected walk: steps +1 (target, no update), -1 floored at 0 (update),
-  // so n_l = max(N + D_l, D_l - min_{k<=l} D_k) with D_l the inclusive step sum. Exclusive part:
-  // mbcnt(pm) - mbcnt(um) = mbcnt(pm) + mbcnt(~um) - lane, one mbcnt chain
-  const uint64_t num = ~um_all;
-  const int32_t d_ex = (int32_t)__builtin_amdgcn_mbcnt_hi(
-      (uint32_t)(num >> 32),
-      __builtin_amdgcn_mbcnt_lo((uint32_t)num, __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)pm, (uint32_t)neg_lane))));
-  const int32_t D = d_ex + (plus ? 1 : (upd ? -1 : 0));
-  const int32_t n_after = max(N + D, D - scan_min(D));
-  const uint64_t bm = __builtin_amdgcn_ballot_w64(plus & (n_after > kMaxSkip));
-  const uint64_t below = (bm - 1) & ~bm;  // lanes before the break (all lanes when none)
-  const int32_t nvalid = min(64, jtop - st + 1);
-  vis += bm ? (uint32_t)__builtin_ctzll(bm) + 1 : (uint32_t)nvalid;
-  const uint64_t um = um_all & below;
-  const int lu = 63 - __builtin_clzll(um | 1);  // last improving lane before the break (when um != 0)
-  const int32_t m_lu = __builtin_amdgcn_readlane(mx, lu);
-  J = um ? jtop - lu : J;
-  M = um ? m_lu : M;
-  const bool wt = ok & (bool)((below >> lane) & 1) & (pj >= 0);
-  __builtin_amdgcn_raw_buffer_store_b32(i, trs, wt ? (uint32_t)pj * 4u : 0xFFFFFFFFu, 0, 0);
-  N = __builtin_amdgcn_readlane(n_after, 63);
-  return bm != 0;
-}
 
 // Producer -> consumer hand-off, one slot per anchor i: the geometry of its first 64 candidates.
 // seq = i + 1 is written last and read first, so a slot whose seq matches is complete.
@@ -168,10 +56,6 @@ struct Slot {
   int32_t seq, st, q_span, pad;
 };
 
-__device__ __forceinline__ uint64_t rfl64_lane(uint64_t v, int l) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32;
-}
 
 // LDS counters are read by every lane; the count is uniform, so take it into an SGPR
 __device__ __forceinline__ int32_t lds_count(int *p) {
@@ -190,19 +74,28 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   __shared__ uint32_t S[kRing + 64];
   __shared__ Slot ring[kSlots];
   __shared__ int consumed;
-  const int c = A.order[blockIdx.x];
+  const VCall &V = A.vc[blockIdx.x];
+  const int c = V.call;
   const int lane = threadIdx.x & 63;
   const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;  // wave-uniform role
-  const int64_t o = A.offsets[c];
-  const int32_t n = __builtin_amdgcn_readfirstlane((int32_t)(A.offsets[c + 1] - o));
+  const int32_t n = V.n, known = V.known;
+  const bool fin = (V.mode & kVFinal) != 0;
+  // parents in memory relative to the call, in registers relative to this block; a parent before the
+  // block (only a fix-up block's loaded anchors have one) lies before every window it computes, so
+  // it reads as "none"
+  const int32_t pbase = V.pbase;
+  auto p_in = [&](int32_t p) { return p >= pbase ? p - pbase : -1; };
   const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
   const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
   const double avg_qspan = (double)A.avg_qspan[c];
-  const uint64_t *X = A.x + o, *Y = A.y + o;
-  int32_t *score = A.score + o, *parent = A.parent + o, *target = A.target + o, *peak = A.peak + o;
+  const uint64_t *X = A.x + V.in, *Y = A.y + V.in;
+  const bool scr = (V.mode & kVScratch) != 0;
+  int32_t *score = (scr ? A.s_score : A.score) + V.out, *parent = (scr ? A.s_parent : A.parent) + V.out;
+  int32_t *target = A.target + V.out, *peak = A.peak + V.out;  // written by kVFinal blocks only
 
   for (int k = threadIdx.x; k < kRing + 64; k += 128) S[k] = 0;
-  for (int32_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
+  if (fin)
+    for (int32_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
   if (threadIdx.x < kSlots) ring[threadIdx.x].seq = 0;
   if (threadIdx.x == 0) consumed = 0;
   __builtin_amdgcn_s_waitcnt(0);  // zeroing stores complete before any later targets store
@@ -212,7 +105,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     // ---------------- producer: geometry of anchor i against i-1-lane --------------------------
     uint64_t wx = 0, wy = 0;  // lane l: anchor i-1-l
     int32_t st = 0;
-    const bool pc = PROF == 2 && c == A.prof_call;
+    const bool pc = PROF == 2 && blockIdx.x == 0;
     unsigned long long p_load = 0, p_wait = 0, t0 = 0;
     // Anchor blocks: bx/by hold X/Y[64b .. 64b+63] (lane k = anchor 64b+k) and the next block is
     // loaded one block ahead, so x[i], y[i] are register reads (readlane), not LDS round trips.
@@ -315,7 +208,8 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   // the LDS latency is hidden). Once f[i-1] and p[i-1] arrive, what is left is lane 0's score (a
   // scalar add), one max + compare per lane for the improvements, lane 0's mark (one bit), and the
   // n_skip walk, which runs in scalar registers over the improvement and target bitmasks.
-  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(target, (short)0, n * 4, 0x00020000);
+  // targets of speculative / fix-up blocks are not written: a zero-sized buffer drops every store
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(target, (short)0, fin ? n * 4 : 0, 0x00020000);
   const int32_t neg_lane = -lane;
   int32_t ws = 0, wpar = -1, wpk = 0;  // lane l: score/parent/peak of anchor i-1-l (top of iteration i)
   unsigned long long vis = 0, n_mem = 0, n_miss = 0, c_pre = 0, c_crit = 0, c_tail = 0, n_walk = 0, c_um = 0, c_walk = 0;
@@ -376,7 +270,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     rt0 = __builtin_amdgcn_s_memrealtime();
     clk0 = __builtin_amdgcn_s_memtime();
   }
-  const bool pc = PROF == 2 && c == A.prof_call;
+  const bool pc = PROF == 2 && blockIdx.x == 0;
   {
     int32_t sg;
     take(0, pst, pq, sg);
@@ -385,6 +279,12 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   int32_t Mprev = 0, Jprev = -1;
   for (int32_t base = 0; base < n; base += 64) {
     const int32_t cnt = min(64, n - base);
+    // kVFixup: anchors < known are final already; their score and parent replace the resolution
+    int32_t kf = 0, kp = -1;
+    if (base < known && base + lane < known) {
+      kf = score[base + lane];
+      kp = p_in(parent[base + lane]);
+    }
     for (int32_t k = 0; k < cnt; k++) {
       const int32_t i = __builtin_amdgcn_readfirstlane(base + k);
       if (PROF >= 1 && (A.exp & 2)) {
@@ -442,7 +342,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       const bool wt = (bool)((okm & below) >> lane & 1) & (pjv >= 0);
       if (!(PROF >= 1 && (A.exp & 32)))
         __builtin_amdgcn_raw_buffer_store_b32(i, trs, wt ? (uint32_t)pjv * 4u : 0xFFFFFFFFu, 0, 0);
-      if (!bm && jtop - 64 >= st) {  // rare: older candidates (j < i-64) from memory
+      if (!bm && jtop - 64 >= st && i >= known) {  // rare: older candidates (j < i-64) from memory
         if (PROF) ++n_mem;
         // this anchor's own stamps first (the next anchor's preparation overwrote them)
         const uint32_t stamp = (uint32_t)(i + 1);
@@ -461,7 +361,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
             xj = X[jj];
             yj = Y[jj];
             scj = load_l2(score + jj);
-            pj = load_l2(parent + jj);
+            pj = p_in(load_l2(parent + jj));
           }
           int32_t sgo;
           const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
@@ -469,6 +369,10 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
                            vis_i))
             break;
         }
+      }
+      if (i < known) {
+        M = __builtin_amdgcn_readlane(kf, k);
+        J = __builtin_amdgcn_readlane(kp, k);
       }
       vis += vis_i;
       unsigned long long t2 = 0;
@@ -479,7 +383,8 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       // peak of the parent: from the register window when J >= i-64, else (rare) from memory
       const int32_t dJ = i - 1 - J;
       int32_t pkJ = __builtin_amdgcn_readlane(wpk, dJ & 63);
-      if (J >= 0 && dJ > 63) pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
+      // (kVFinal only: other blocks keep no peaks, and their `out` is not an offset into `peak`)
+      if (fin && J >= 0 && dJ > 63) pkJ = __builtin_amdgcn_readfirstlane(load_l2(peak + J));
       const int32_t pki = (PROF >= 1 && (A.exp & 64)) ? M : (J >= 0 && pkJ > M) ? pkJ : M;
       ws = lane == 0 ? M : ws1;
       wpar = lane == 0 ? J : wp1;
@@ -489,17 +394,17 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
       if (pc) c_tail += __builtin_amdgcn_s_memtime() - t2;
     }
     // flush the window: anchors base .. base+cnt-1 (lane l: base+cnt-1-l)
-    if (lane < cnt) {
+    if (lane < cnt && base + cnt - 1 - lane >= known) {
       score[base + cnt - 1 - lane] = ws;
-      parent[base + cnt - 1 - lane] = wpar;
-      peak[base + cnt - 1 - lane] = wpk;
+      parent[base + cnt - 1 - lane] = wpar >= 0 ? wpar + pbase : -1;
+      if (fin) peak[base + cnt - 1 - lane] = wpk;
     }
   }
   if (PROF && lane == 0) {
     const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
     atomicMin(A.prof + 8, rt0);
     atomicMax(A.prof + 11, rt1);
-    if (c == A.prof_call) {
+    if (blockIdx.x == 0) {
       atomicAdd(A.prof + 9, rt0);
       atomicAdd(A.prof + 10, rt1);
       atomicAdd(A.prof + 0, c_pre);
@@ -515,7 +420,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     }
   }
   // every lane accumulated the same (uniform) count
-  if (lane == 0) atomicAdd(A.visited, vis);
+  if (fin && lane == 0) atomicAdd(A.visited, vis);
 }
 
 }  // namespace gbchain
@@ -541,12 +446,6 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
                const int32_t *params4, const uint64_t *x, const uint64_t *y) {
   if (int st = validate(ncalls, offsets, avg_qspan, params4, x, y)) return st;
   const int64_t na = offsets[ncalls];
-  // longest calls first: the grid is dispatched in order, so the critical path starts first
-  std::vector<int32_t> order((size_t)ncalls);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-    return offsets[a + 1] - offsets[a] > offsets[b + 1] - offsets[b];
-  });
   GB_HIP(hipSetDevice(B->device));
   GB_HIP(hipStreamSynchronize(B->stream));  // the previous contents may still be in use
   gbchain::chain_bt_destroy(B->bt);
@@ -554,13 +453,12 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
   B->ran = false;
   const int64_t nc = std::max<int64_t>(ncalls, 1), nn = std::max<int64_t>(na, 1);
   if (nc > B->cap_calls) {
-    for (void *q : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order}) (void)hipFree(q);
-    B->d_off = nullptr, B->d_aq = nullptr, B->d_par4 = nullptr, B->d_order = nullptr;
+    for (void *q : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4}) (void)hipFree(q);
+    B->d_off = nullptr, B->d_aq = nullptr, B->d_par4 = nullptr;
     B->cap_calls = 0;
     GB_HIP(hipMalloc(&B->d_off, (size_t)(nc + 1) * sizeof(int64_t)));
     GB_HIP(hipMalloc(&B->d_aq, (size_t)nc * sizeof(float)));
     GB_HIP(hipMalloc(&B->d_par4, (size_t)nc * 4 * sizeof(int32_t)));
-    GB_HIP(hipMalloc(&B->d_order, (size_t)nc * sizeof(int32_t)));
     B->cap_calls = nc;
   }
   if (nn > B->cap_anchors) {
@@ -578,15 +476,49 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
   if (ncalls) {
     GB_HIP(hipMemcpy(B->d_aq, avg_qspan, (size_t)ncalls * sizeof(float), hipMemcpyHostToDevice));
     GB_HIP(hipMemcpy(B->d_par4, params4, (size_t)ncalls * 16, hipMemcpyHostToDevice));
-    GB_HIP(hipMemcpy(B->d_order, order.data(), (size_t)ncalls * 4, hipMemcpyHostToDevice));
   }
   if (na) {
     GB_HIP(hipMemcpy(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice));
     GB_HIP(hipMemcpy(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice));
   }
-  return GB_OK;
+  // the block table: whole calls, or long calls as speculative segments (chain_split.hip)
+  return gbchain::split_plan(B, offsets, x, params4);
 }
 
+}  // namespace
+
+namespace gbchain {
+// One launch of the sequential kernel over nvc blocks of the block table d_vc.
+int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof) {
+  if (nvc <= 0) return GB_OK;
+  Args A;
+  A.vc = d_vc;
+  A.avg_qspan = B->d_aq;
+  A.params4 = B->d_par4;
+  A.x = B->d_x;
+  A.y = B->d_y;
+  const size_t nn = (size_t)std::max<int64_t>(B->nanchors, 1);
+  A.score = B->d_out;
+  A.parent = B->d_out + nn;
+  A.target = B->d_out + 2 * nn;
+  A.peak = B->d_out + 3 * nn;
+  A.s_score = B->d_sscore;
+  A.s_parent = B->d_sparent;
+  A.visited = B->d_vis;
+  A.prof = prof ? B->d_prof : nullptr;
+  A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
+  if (prof == 2)
+    hipLaunchKernelGGL(chain_kernel<2>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
+  else if (prof == 1)
+    hipLaunchKernelGGL(chain_kernel<1>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
+  else
+    hipLaunchKernelGGL(chain_kernel<0>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
+  GB_HIP(hipGetLastError());
+  return GB_OK;
+}
+}  // namespace gbchain
+
+namespace {
 int batch_new(gb_chain_batch **out) {
   auto *B = new gb_chain_batch();
   hipError_t e = hipGetDevice(&B->device);
@@ -632,40 +564,19 @@ int gb_chain_batch_run(gb_chain_batch *B) {
   GB_HIP(hipMemsetAsync(B->d_vis, 0, sizeof(unsigned long long), B->stream));
   GB_HIP(hipEventRecord(B->ev[0], B->stream));
   if (B->ncalls > 0) {
-    gbchain::Args A;
-    A.offsets = B->d_off;
-    A.avg_qspan = B->d_aq;
-    A.params4 = B->d_par4;
-    A.x = B->d_x;
-    A.y = B->d_y;
-    A.order = B->d_order;
-    const size_t nn = (size_t)std::max<int64_t>(B->nanchors, 1);
-    A.score = B->d_out;
-    A.parent = B->d_out + nn;
-    A.target = B->d_out + 2 * nn;
-    A.peak = B->d_out + 3 * nn;
-    A.visited = B->d_vis;
-    A.prof = nullptr;
-    A.prof_call = -1;
-    A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
     const char *pe = getenv("GB_CHAIN_PROF");
     const int prof = (pe && (*pe == '1' || *pe == '2')) ? *pe - '0' : 0;
     if (prof) {
       if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 16 * sizeof(unsigned long long)));
       GB_HIP(hipMemsetAsync(B->d_prof, 0, 16 * sizeof(unsigned long long), B->stream));
       GB_HIP(hipMemsetAsync(B->d_prof + 8, 0xff, sizeof(unsigned long long), B->stream));
-      A.prof = B->d_prof;
-      int32_t c0 = 0;
-      GB_HIP(hipMemcpy(&c0, B->d_order, sizeof(c0), hipMemcpyDeviceToHost));
-      A.prof_call = c0;
     }
-    if (prof == 2)
-      hipLaunchKernelGGL(gbchain::chain_kernel<2>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
-    else if (prof == 1)
-      hipLaunchKernelGGL(gbchain::chain_kernel<1>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
-    else
-      hipLaunchKernelGGL(gbchain::chain_kernel<0>, dim3((unsigned)B->ncalls), dim3(128), 0, B->stream, A);
-    GB_HIP(hipGetLastError());
+    // split calls: their targets past segment 0 are marked later by atomic max over zeros
+    if (!B->split.empty())
+      GB_HIP(hipMemsetAsync(B->d_out + 2 * std::max<int64_t>(B->nanchors, 1), 0, (size_t)B->nanchors * 4, B->stream));
+    if (int st = gbchain::launch_chain(B, B->d_vc, (int)B->vc.size(), prof)) return st;
+    if (!B->split.empty())
+      if (int st = gbchain::split_resolve(B)) return st;
   }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   if (B->d_prof && getenv("GB_CHAIN_PROF")) {
@@ -680,6 +591,14 @@ int gb_chain_batch_run(gb_chain_batch *B) {
             (double)(h[10] - h[8]) * 1e-5, h[14], h[15], h[12], h[13]);
   }
   B->ran = true;
+  return GB_OK;
+}
+
+int gb_chain_batch_split_stats(gb_chain_batch *B, int64_t *split_calls, int64_t *rounds, int64_t *fixups) {
+  GB_ARG(B, "gb_chain_batch_split_stats: null batch");
+  if (split_calls) *split_calls = (int64_t)B->split.size();
+  if (rounds) *rounds = B->spec_rounds;
+  if (fixups) *fixups = B->fixups;
   return GB_OK;
 }
 
@@ -719,7 +638,8 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
   if (!B) return GB_OK;
   if (B->stream) (void)hipStreamSynchronize(B->stream);
   gbchain::chain_bt_destroy(B->bt);
-  for (void *p : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_order, (void *)B->d_x,
+  gbchain::split_free(B);
+  for (void *p : {(void *)B->d_off, (void *)B->d_aq, (void *)B->d_par4, (void *)B->d_x,
                   (void *)B->d_y, (void *)B->d_out, (void *)B->d_vis, (void *)B->d_prof})
     (void)hipFree(p);
   for (auto ev : B->ev)

@@ -1,0 +1,512 @@
+// chain_split.hip -- long chain_dp calls as speculative segments, resolved exactly.
+//
+// chain_dp (minimap2-acceleration kernel/scalar/src/host_kernel.cpp:30-94) is sequential in the
+// anchors of a call: score[i] needs score[j] for j in i's window. One call per block makes the
+// longest call the bound of a whole set (an 87 k-anchor call takes as long as 10 000 calls). A call
+// of >= 2 * kSeg anchors whose x are sorted (minimap2 sorts them) is therefore cut into segments
+// [c_s, e_s) of kSeg anchors, and segment s >= 1 runs as its own block from a warm-up anchor a_s
+// before its window (a_s = st(c_s) - kWarm: with sorted x the window start st(i) is a function of
+// i alone, max(first j with x_i <= x_j + max_dist_x, i - max_iter), so the segment's loops see
+// exactly the reference's candidates). Its scores are then off by the unknown score of the chains
+// it continues, so:
+//
+//  1. guess: score[i] ~ score[p] + (spec[i] - spec[p]) along the speculative parents p, resolved by
+//     pointer jumping back to a known score (segment 0 is exact) or a chain start;
+//  2. verify: every anchor's loop is re-run in parallel (one wave per 64 anchors) against the
+//     guessed scores and parents of its window; by induction over i, an anchor whose loop yields
+//     its own guess is exact as long as all earlier anchors are, so the first mismatch bounds what
+//     is final;
+//  3. fix-up: from a mismatch, kFix anchors are recomputed by the sequential kernel with the final
+//     anchors before them loaded (kVFixup), and 1-2 repeat from there (rare: the chains of the
+//     warm-up have converged to the reference's well before c_s on the data measured);
+//  4. peaks by pointer jumping (peak[i] = max(score[i], peak[parent[i]])), then the targets marks
+//     and visited counts of the split anchors by one more parallel pass (atomic max: the last
+//     marker of an anchor is the largest i).
+//
+// The results are those of the sequential loop, bit for bit; tests/test_chain.py forces tiny
+// segments and no warm-up to drive every fix-up path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../include/gb_chain.h"
+#include "gb_common.h"
+#include "chain_dev.h"
+#include "chain_internal.h"
+
+namespace gbchain {
+
+constexpr int kSegDefault = 4096;   // segment length
+constexpr int kWarmDefault = 256;   // warm-up anchors before the window of a segment's first anchor
+constexpr int kFix = 1024;          // anchors recomputed sequentially after a failed guess
+constexpr int kTagRing = 1024;      // verification stamp ring (tagged, see resolve_tagged)
+
+struct SplitArgs {
+  const SplitCall *split;
+  const Seg *segs;
+  const Chunk *chunks;
+  const int32_t *st;
+  const int32_t *front;
+  int32_t *fail;
+  const float *avg_qspan;
+  const int32_t *params4;
+  const uint64_t *x, *y;
+  int32_t *score, *parent, *target, *peak;
+  const int32_t *s_score, *s_parent;
+  unsigned long long *visited;
+  int32_t fault;  // GB_CHAIN_SPLIT_FAULT (tests): guesses of every fault-th anchor are made wrong
+};
+
+__device__ __forceinline__ int32_t cidx(const SplitCall &S, int32_t i) { return 64 * S.cbase + (i - S.c1); }
+
+// 1. guess: per split anchor i >= front, its speculative parent p and the link / value pair of
+// g[i] = g[link] + val (link -1: val is g[i]).
+__global__ __launch_bounds__(64) void guess_init(SplitArgs A, int32_t *link, int32_t *val) {
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall S = A.split[ch.sc];
+  const int32_t i = ch.start + (int32_t)threadIdx.x, j = 64 * blockIdx.x + threadIdx.x;
+  const int32_t front = A.front[ch.sc];
+  if (i >= S.n || i < front) {
+    link[j] = -1;
+    val[j] = 0;
+    return;
+  }
+  const int32_t s = min(i / S.c1, S.nseg - 1);  // segments are c1 anchors long, the last one longer
+  const Seg G = A.segs[S.seg0 + s];
+  const int32_t fs = A.s_score[G.soff + (i - G.as)], q = A.s_parent[G.soff + (i - G.as)];
+  const int32_t p = q >= 0 ? q + G.as : -1;
+  A.parent[S.off + i] = p;
+  int32_t l = -1, v = fs;
+  if (p >= 0) {
+    const int32_t d = fs - A.s_score[G.soff + (p - G.as)];
+    if (p < front) {
+      v = A.score[S.off + p] + d;
+    } else {
+      l = cidx(S, p);
+      v = d;
+    }
+  }
+  // fault injection (tests only): a wrong guess must be caught by the verification and repaired
+  // by the fix-up, whatever the spec run found
+  if (A.fault > 0 && i % A.fault == A.fault / 2) v += 1;
+  link[j] = l;
+  val[j] = v;
+}
+
+// one pointer-jumping round: OP 0 adds (guesses), OP 1 takes the maximum (peaks)
+template <int OP>
+__global__ __launch_bounds__(256) void jump_round(int64_t n, const int32_t *li, const int32_t *vi, int32_t *lo,
+                                                  int32_t *vo) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int32_t l = li[j];
+  int32_t v = vi[j];
+  if (l >= 0) {
+    v = OP == 0 ? v + vi[l] : max(v, vi[l]);
+    lo[j] = li[l];
+  } else {
+    lo[j] = -1;
+  }
+  vo[j] = v;
+}
+
+__global__ __launch_bounds__(64) void guess_write(SplitArgs A, const int32_t *val) {
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall S = A.split[ch.sc];
+  const int32_t i = ch.start + (int32_t)threadIdx.x;
+  if (i < S.n && i >= A.front[ch.sc]) A.score[S.off + i] = val[64 * blockIdx.x + threadIdx.x];
+}
+
+// 4. peaks: peak[i] = parent >= 0 && peak[parent] > score[i] ? peak[parent] : score[i]
+// (host_kernel.cpp:92), i.e. the maximum score on i's parent path; segment 0's peaks are final.
+__global__ __launch_bounds__(64) void peak_init(SplitArgs A, int32_t *link, int32_t *val) {
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall S = A.split[ch.sc];
+  const int32_t i = ch.start + (int32_t)threadIdx.x, j = 64 * blockIdx.x + threadIdx.x;
+  if (i >= S.n) {
+    link[j] = -1;
+    val[j] = 0;
+    return;
+  }
+  const int32_t f = A.score[S.off + i], p = A.parent[S.off + i];
+  int32_t l = -1, v = f;
+  if (p >= S.c1)
+    l = cidx(S, p);
+  else if (p >= 0)
+    v = max(f, A.peak[S.off + p]);
+  link[j] = l;
+  val[j] = v;
+}
+
+// The verification ring: a mark is the anchor's index within the chunk (k + 1, 7 bits) tagged with
+// the position's bits above the ring size, so positions that share a slot are told apart; a mark
+// that would overwrite another mark of the same anchor at a different position (the ring is
+// smaller than max_iter) is a conflict, and the anchor is not verified (it goes to the fix-up).
+__device__ __forceinline__ uint32_t ring_tag(int k, int32_t pos) {
+  return (uint32_t)(k + 1) | ((uint32_t)pos >> 10 << 7);
+}
+
+template <int MARK>
+__device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, int k,
+                                               int lane, int32_t neg_lane, uint32_t *S, int32_t &M, int32_t &J,
+                                               int32_t &N, uint32_t &vis, bool &conflict, int32_t *tgt, int32_t i) {
+  const bool writer = ok & (pj >= st);
+  const uint32_t slot = writer ? (uint32_t)(pj & (kTagRing - 1)) : (uint32_t)(kTagRing + lane);
+  const uint32_t tw = ring_tag(k, pj);
+  const uint32_t prev = S[slot];
+  conflict |= writer & ((prev & 127u) == (uint32_t)(k + 1)) & (prev != tw);
+  S[slot] = tw;
+  conflict |= writer & (S[slot] != tw);
+  const int32_t j = jtop - lane;
+  const bool tg = S[j & (kTagRing - 1)] == ring_tag(k, j);
+  const int32_t mx = scan_max(sc);
+  const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
+  const bool upd = sc > before;
+  const bool plus = ok & !upd & tg;
+  const uint64_t um_all = __builtin_amdgcn_ballot_w64(upd), pm = __builtin_amdgcn_ballot_w64(plus);
+  const uint64_t num = ~um_all;
+  const int32_t d_ex = (int32_t)__builtin_amdgcn_mbcnt_hi(
+      (uint32_t)(num >> 32),
+      __builtin_amdgcn_mbcnt_lo((uint32_t)num, __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)pm, (uint32_t)neg_lane))));
+  const int32_t D = d_ex + (plus ? 1 : (upd ? -1 : 0));
+  const int32_t n_after = max(N + D, D - scan_min(D));
+  const uint64_t bm = __builtin_amdgcn_ballot_w64(plus & (n_after > kMaxSkip));
+  const uint64_t below = (bm - 1) & ~bm;
+  const int32_t nvalid = min(64, jtop - st + 1);
+  vis += bm ? (uint32_t)__builtin_ctzll(bm) + 1 : (uint32_t)max(nvalid, 0);
+  const uint64_t um = um_all & below;
+  const int lu = 63 - __builtin_clzll(um | 1);
+  const int32_t m_lu = __builtin_amdgcn_readlane(mx, lu);
+  J = um ? jtop - lu : J;
+  M = um ? m_lu : M;
+  if (MARK && ok && ((below >> lane) & 1) && pj >= 0) atomicMax(tgt + pj, i);
+  N = __builtin_amdgcn_readlane(n_after, 63);
+  return bm != 0;
+}
+
+// 2. verify (MARK 0): re-run the loop of every split anchor i >= front against the guessed window;
+// fail[sc] = the first i whose loop does not give its own guess. MARK 1 (after convergence): the
+// same loops over all split anchors write the targets marks, count the visited pairs and store the
+// peaks resolved in `pv`.
+template <int MARK>
+__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const int32_t *pv) {
+  __shared__ uint32_t S[kTagRing + 64];
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall Sc = A.split[ch.sc];
+  const int lane = threadIdx.x;
+  const int32_t start = ch.start, n = Sc.n;
+  const int32_t front = MARK ? Sc.c1 : A.front[ch.sc];
+  const int32_t cnt = min(64, n - start);
+  if (start + cnt <= front) return;
+  const int c = Sc.call;
+  const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
+  const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
+  const double avg_qspan = (double)A.avg_qspan[c];
+  const uint64_t *X = A.x + Sc.off, *Y = A.y + Sc.off;
+  const int32_t *score = A.score + Sc.off, *parent = A.parent + Sc.off;
+  int32_t *tgt = A.target + Sc.off;
+  for (int t = lane; t < kTagRing + 64; t += 64) S[t] = 0;
+  // window: lane l = anchor start-1-l; the chunk's anchors: lane l = start+l
+  const int32_t j0 = start - 1 - lane;
+  uint64_t wx = 0, wy = 0;
+  int32_t wf = 0, wp = -1;
+  if (j0 >= 0) {
+    wx = X[j0];
+    wy = Y[j0];
+    wf = score[j0];
+    wp = parent[j0];
+  }
+  const int32_t ci = min(start + lane, n - 1);
+  const uint64_t bx = X[ci], by = Y[ci];
+  const int32_t bf = score[ci], bp = parent[ci], bst = A.st[64 * blockIdx.x + lane];
+  const int32_t neg_lane = -lane;
+  uint32_t vis = 0;
+  int32_t first_bad = INT_MAX;
+  for (int k = 0; k < cnt; k++) {
+    const int32_t i = start + k;
+    const uint64_t xi = rfl64_lane(bx, k), yi = rfl64_lane(by, k);
+    const int32_t fi = __builtin_amdgcn_readlane(bf, k), pi = __builtin_amdgcn_readlane(bp, k);
+    if (i >= front) {
+      const int32_t st = __builtin_amdgcn_readlane(bst, k);
+      int32_t sg;
+      const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+      int32_t M = (int32_t)(yi >> 32 & 0xff), J = -1, N = 0;
+      bool conflict = false;
+      bool broke = resolve_tagged<MARK>(ok ? sg + wf : INT_MIN, ok, wp, i - 1, st, k, lane, neg_lane, S, M, J, N,
+                                        vis, conflict, tgt, i);
+      for (int32_t jt = i - 65; !broke && jt >= st; jt -= 64) {  // older candidates from memory
+        const int32_t jj = jt - lane;
+        const bool v = jj >= st;
+        uint64_t xj = 0, yj = 0;
+        int32_t fj = 0, pj = -1;
+        if (v) {
+          xj = X[jj];
+          yj = Y[jj];
+          fj = score[jj];
+          pj = parent[jj];
+        }
+        int32_t sgo;
+        const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
+        broke = resolve_tagged<MARK>(oko ? sgo + fj : INT_MIN, oko, pj, jt, st, k, lane, neg_lane, S, M, J, N, vis,
+                                     conflict, tgt, i);
+      }
+      const bool clash = __builtin_amdgcn_ballot_w64(conflict) != 0;
+      if (!MARK && (M != fi || J != pi || clash) && first_bad == INT_MAX) first_bad = i;
+    }
+    wx = dpp_shr_u64(wx, xi);
+    wy = dpp_shr_u64(wy, yi);
+    wf = dpp_shr_i32(wf, fi);
+    wp = dpp_shr_i32(wp, pi);
+  }
+  if (!MARK) {
+    if (lane == 0 && first_bad != INT_MAX) atomicMin(A.fail + ch.sc, first_bad);
+  } else {
+    if (lane < cnt) A.peak[Sc.off + start + lane] = pv[64 * blockIdx.x + lane];
+    if (lane == 0) atomicAdd(A.visited, (unsigned long long)vis);
+  }
+}
+
+namespace {
+
+template <typename T>
+int grow(T **p, int64_t *cap, int64_t need) {
+  need = std::max<int64_t>(need, 1);
+  if (need <= *cap) return GB_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  GB_HIP(hipMalloc(p, (size_t)need * sizeof(T)));
+  *cap = need;
+  return GB_OK;
+}
+
+// GB_CHAIN_SPLIT: "0" runs every call whole; "SEG[,WARM]" sets the segment length and warm-up
+// (tests force tiny segments without warm-up to exercise the fix-up path).
+void split_knobs(int *seg, int *warm) {
+  *seg = kSegDefault;
+  *warm = kWarmDefault;
+  const char *e = getenv("GB_CHAIN_SPLIT");
+  if (!e || !*e) return;
+  int a = 0, b = -1;
+  const int k = sscanf(e, "%d,%d", &a, &b);
+  if (k >= 1) *seg = a;
+  if (k >= 2 && b >= 0) *warm = b;
+}
+
+SplitArgs split_args(gb_chain_batch *B) {
+  SplitArgs A;
+  const size_t nn = (size_t)std::max<int64_t>(B->nanchors, 1);
+  A.split = B->d_split;
+  A.segs = B->d_segs;
+  A.chunks = B->d_chunks;
+  A.st = B->d_st;
+  A.front = B->d_front;
+  A.fail = B->d_fail;
+  A.avg_qspan = B->d_aq;
+  A.params4 = B->d_par4;
+  A.x = B->d_x;
+  A.y = B->d_y;
+  A.score = B->d_out;
+  A.parent = B->d_out + nn;
+  A.target = B->d_out + 2 * nn;
+  A.peak = B->d_out + 3 * nn;
+  A.s_score = B->d_sscore;
+  A.s_parent = B->d_sparent;
+  A.visited = B->d_vis;
+  const char *f = getenv("GB_CHAIN_SPLIT_FAULT");
+  A.fault = f ? atoi(f) : 0;
+  return A;
+}
+
+// ceil(log2(n)) + 1 rounds resolve any parent path of n anchors
+int jump_rounds(int n) {
+  int r = 1;
+  while ((1ll << (r - 1)) < (int64_t)n) r++;
+  return r;
+}
+
+// pointer jumping from buffers 0; returns the buffer index holding the result
+int jump(gb_chain_batch *B, int op, int rounds) {
+  const int64_t nj = 64 * (int64_t)B->chunks.size();
+  const unsigned g = (unsigned)((nj + 255) / 256);
+  int cur = 0;
+  for (int r = 0; r < rounds; r++) {
+    if (op == 0)
+      hipLaunchKernelGGL(jump_round<0>, dim3(g), dim3(256), 0, B->stream, nj, B->d_link[cur], B->d_val[cur],
+                         B->d_link[cur ^ 1], B->d_val[cur ^ 1]);
+    else
+      hipLaunchKernelGGL(jump_round<1>, dim3(g), dim3(256), 0, B->stream, nj, B->d_link[cur], B->d_val[cur],
+                         B->d_link[cur ^ 1], B->d_val[cur ^ 1]);
+    cur ^= 1;
+  }
+  return cur;
+}
+
+}  // namespace
+
+int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4) {
+  int seg, warm;
+  split_knobs(&seg, &warm);
+  const int64_t ncalls = B->ncalls;
+  B->vc.clear();
+  B->split.clear();
+  B->segs.clear();
+  B->chunks.clear();
+  B->st.clear();
+  B->scratch_n = 0;
+  B->max_split_n = 0;
+  std::vector<int32_t> stw;
+  for (int64_t c = 0; c < ncalls; c++) {
+    const int64_t off = offsets[c];
+    const int32_t n = (int32_t)(offsets[c + 1] - off);
+    bool split = seg >= 64 && (int64_t)n >= 2 * (int64_t)seg;
+    for (int32_t i = 1; split && i < n; i++) split = x[off + i] >= x[off + i - 1];
+    // the chunk space (64 * chunks) is indexed with int32
+    if (split && 64 * ((int64_t)B->chunks.size() + n / 64 + 1) >= INT32_MAX) split = false;
+    if (!split) {
+      B->vc.push_back({off, off, n, (int32_t)c, 0, kVFinal, 0, 0});
+      continue;
+    }
+    // st(i) as the reference's loop walks it (host_kernel.cpp:57-58)
+    stw.resize((size_t)n);
+    const uint64_t mdx = (uint64_t)(int64_t)params4[4 * c];
+    int32_t s = 0;
+    for (int32_t i = 0; i < n; i++) {
+      while (s < i && x[off + i] > x[off + s] + mdx) ++s;
+      if (i - s > kMaxIter) s = i - kMaxIter;
+      stw[(size_t)i] = s;
+    }
+    SplitCall S;
+    S.off = off;
+    S.n = n;
+    S.call = (int32_t)c;
+    S.seg0 = (int32_t)B->segs.size();
+    S.nseg = n / seg;
+    S.c1 = seg;
+    S.cbase = (int32_t)B->chunks.size();
+    B->vc.push_back({off, off, seg, (int32_t)c, 0, kVFinal, 0, 0});  // segment 0: exact
+    B->segs.push_back({0, seg, 0, 0, -1});
+    for (int32_t k = 1; k < S.nseg; k++) {
+      Seg G;
+      G.cs = k * seg;
+      G.es = k + 1 == S.nseg ? n : (k + 1) * seg;
+      G.as = std::max(0, stw[(size_t)G.cs] - warm);
+      G.pad = 0;
+      G.soff = B->scratch_n;
+      B->scratch_n += G.es - G.as;
+      B->vc.push_back({off + G.as, G.soff, G.es - G.as, (int32_t)c, 0, kVScratch, 0, 0});
+      B->segs.push_back(G);
+    }
+    const int32_t sc = (int32_t)B->split.size();
+    for (int32_t st0 = S.c1; st0 < n; st0 += 64) B->chunks.push_back({sc, st0});
+    B->st.resize(64 * B->chunks.size(), 0);
+    for (int32_t i = S.c1; i < n; i++) B->st[(size_t)64 * S.cbase + (size_t)(i - S.c1)] = stw[(size_t)i];
+    B->split.push_back(S);
+    B->max_split_n = std::max(B->max_split_n, n);
+  }
+  // longest blocks first: the grid is dispatched in order, so the critical paths start first
+  std::stable_sort(B->vc.begin(), B->vc.end(), [](const VCall &a, const VCall &b) { return a.n > b.n; });
+  const int64_t nvc = (int64_t)B->vc.size();
+  // room for one fix-up block per split call behind the table (split_resolve)
+  if (int st = grow(&B->d_vc, &B->cap_vc, nvc + (int64_t)B->split.size())) return st;
+  if (nvc) GB_HIP(hipMemcpy(B->d_vc, B->vc.data(), (size_t)nvc * sizeof(VCall), hipMemcpyHostToDevice));
+  if (B->split.empty()) return GB_OK;
+  const int64_t ns = (int64_t)B->split.size(), nch = (int64_t)B->chunks.size();
+  int st = grow(&B->d_split, &B->cap_split, ns);
+  if (!st) st = grow(&B->d_segs, &B->cap_segs, (int64_t)B->segs.size());
+  if (!st) st = grow(&B->d_chunks, &B->cap_chunks, nch);
+  if (!st) st = grow(&B->d_st, &B->cap_st, 64 * nch);
+  if (!st) st = grow(&B->d_sscore, &B->cap_sscore, B->scratch_n);
+  if (!st) st = grow(&B->d_sparent, &B->cap_sparent, B->scratch_n);
+  if (!st) st = grow(&B->d_front, &B->cap_front, 2 * ns);
+  if (st) return st;
+  B->d_fail = B->d_front + ns;
+  {
+    const int64_t need = 64 * nch;
+    if (need > B->cap_jump) {
+      for (int k = 0; k < 2; k++) {
+        (void)hipFree(B->d_link[k]);
+        (void)hipFree(B->d_val[k]);
+        B->d_link[k] = B->d_val[k] = nullptr;
+      }
+      B->cap_jump = 0;
+      for (int k = 0; k < 2; k++) {
+        GB_HIP(hipMalloc(&B->d_link[k], (size_t)need * sizeof(int32_t)));
+        GB_HIP(hipMalloc(&B->d_val[k], (size_t)need * sizeof(int32_t)));
+      }
+      B->cap_jump = need;
+    }
+  }
+  GB_HIP(hipMemcpy(B->d_split, B->split.data(), (size_t)ns * sizeof(SplitCall), hipMemcpyHostToDevice));
+  GB_HIP(hipMemcpy(B->d_segs, B->segs.data(), B->segs.size() * sizeof(Seg), hipMemcpyHostToDevice));
+  GB_HIP(hipMemcpy(B->d_chunks, B->chunks.data(), (size_t)nch * sizeof(Chunk), hipMemcpyHostToDevice));
+  GB_HIP(hipMemcpy(B->d_st, B->st.data(), (size_t)64 * nch * sizeof(int32_t), hipMemcpyHostToDevice));
+  return GB_OK;
+}
+
+int split_resolve(gb_chain_batch *B) {
+  gb::Range range_("gb.chain.split_resolve");
+  const int64_t ns = (int64_t)B->split.size();
+  const unsigned nch = (unsigned)B->chunks.size();
+  std::vector<int32_t> front((size_t)ns), fail((size_t)ns);
+  for (int64_t k = 0; k < ns; k++) front[(size_t)k] = B->split[(size_t)k].c1;
+  GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
+  const SplitArgs A = split_args(B);
+  const int rounds = jump_rounds(B->max_split_n);
+  std::vector<VCall> fix;
+  B->spec_rounds = 0;
+  B->fixups = 0;
+  while (true) {
+    B->spec_rounds++;
+    hipLaunchKernelGGL(guess_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
+    const int r = jump(B, 0, rounds);
+    hipLaunchKernelGGL(guess_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+    GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
+    hipLaunchKernelGGL(verify_kernel<0>, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)nullptr);
+    GB_HIP(hipGetLastError());
+    GB_HIP(hipMemcpyAsync(fail.data(), B->d_fail, (size_t)ns * 4, hipMemcpyDeviceToHost, B->stream));
+    GB_HIP(hipStreamSynchronize(B->stream));
+    fix.clear();
+    for (int64_t k = 0; k < ns; k++) {
+      const int32_t f = fail[(size_t)k];
+      if (f == 0x7f7f7f7f) {
+        front[(size_t)k] = B->split[(size_t)k].n;
+        continue;
+      }
+      const SplitCall &S = B->split[(size_t)k];
+      const int32_t a0 = B->st[(size_t)64 * S.cbase + (size_t)(f - S.c1)];
+      const int32_t e = std::min<int32_t>(S.n, f + kFix);
+      fix.push_back({S.off + a0, S.off + a0, e - a0, S.call, f - a0, kVFixup, a0, 0});
+      front[(size_t)k] = e;
+    }
+    if (fix.empty()) break;
+    B->fixups += (int64_t)fix.size();
+    // fix-up blocks go behind the block table (split_plan left room for one per split call)
+    VCall *d_fix = B->d_vc + B->vc.size();
+    GB_HIP(hipMemcpyAsync(d_fix, fix.data(), fix.size() * sizeof(VCall), hipMemcpyHostToDevice, B->stream));
+    if (int st = launch_chain(B, d_fix, (int)fix.size(), 0)) return st;
+    GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
+    GB_HIP(hipStreamSynchronize(B->stream));  // the host vectors are reused next round
+  }
+  hipLaunchKernelGGL(peak_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
+  const int r = jump(B, 1, rounds);
+  hipLaunchKernelGGL(verify_kernel<1>, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+  GB_HIP(hipGetLastError());
+  return GB_OK;
+}
+
+void split_free(gb_chain_batch *B) {
+  for (void *p : {(void *)B->d_vc, (void *)B->d_split, (void *)B->d_segs, (void *)B->d_chunks, (void *)B->d_st,
+                  (void *)B->d_sscore, (void *)B->d_sparent, (void *)B->d_front, (void *)B->d_link[0],
+                  (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1]})
+    (void)hipFree(p);
+  B->d_vc = nullptr;
+}
+
+}  // namespace gbchain

@@ -36,6 +36,12 @@ int gb_chain_batch_sync(gb_chain_batch *b);
 int gb_chain_batch_results(gb_chain_batch *b, int32_t *scores, int32_t *parents, int32_t *targets,
                            int32_t *peak_scores, int64_t *visited);
 int gb_chain_batch_timing(gb_chain_batch *b, float *kernel_ms);
+/* Diagnostics of the last run: calls run as speculative segments (long calls with sorted x, see
+ * csrc/chain_split.hip), guess/verify rounds, and fix-up blocks (anchors whose guess failed the
+ * verification and were recomputed sequentially). Environment (development aids, read when a batch
+ * is filled): GB_CHAIN_SPLIT = "0" (no splitting) or "SEG[,WARM]"; GB_CHAIN_SPLIT_FAULT = k makes
+ * the guess of every k-th anchor wrong (read at run time), to exercise the verification. */
+int gb_chain_batch_split_stats(gb_chain_batch *b, int64_t *split_calls, int64_t *rounds, int64_t *fixups);
 int gb_chain_batch_destroy(gb_chain_batch *b);
 
 /* Chain backtrack on the batch's chain_dp outputs (asynchronous): minimap2's consumer of score /

@@ -96,3 +96,72 @@ def test_gpu_cli_dropin(golden, tmp_path):
             sc.append(int(a))
             par.append(int(b))
     assert (np.array(sc) == exp[0]).all() and (np.array(par) == exp[1]).all()
+
+
+def _concat_calls(parts):
+    offs = [0]
+    for p in parts:
+        offs.extend((offs[-1] + p.offsets[1:]).tolist())
+    return gen.ChainCalls(np.array(offs, np.int64), np.concatenate([p.x for p in parts]),
+                          np.concatenate([p.y for p in parts]), np.concatenate([p.avg_qspan for p in parts]),
+                          np.concatenate([p.params4 for p in parts]))
+
+
+def _cloud_call(rng, n, diagonals, spread, step, noise, span=15):
+    """Dense anchors on a few parallel noisy diagonals (competing chains in every window)."""
+    x = (np.cumsum(rng.integers(step[0], step[1] + 1, n)) + 1000).astype(np.uint64)
+    offs = rng.integers(-spread, spread, diagonals)
+    y = np.maximum(x.astype(np.int64) + offs[rng.integers(0, diagonals, n)] + rng.integers(-noise, noise + 1, n), 0)
+    yy = (np.uint64(span) << np.uint64(32)) | y.astype(np.uint64)
+    return gen.ChainCalls(np.array([0, n]), x, yy, np.array([15.0], np.float32),
+                          np.array([[5000, 5000, 500, 1]], np.int32))
+
+
+def split_set(seed):
+    """Long minimap2-shaped calls, dense multi-diagonal clouds (windows of > 1 000 anchors) and one
+    long call with unsorted x (never split), for the speculative-segment path."""
+    rng = np.random.default_rng(seed)
+    parts = [gen.chain_dataset("small", num_calls=40, seed=seed, median_n=3000, max_n=40000)]
+    parts.append(_cloud_call(rng, 12000, 4, 300, (1, 6), 3))
+    parts.append(_cloud_call(rng, 9000, 16, 450, (0, 2), 3))
+    u = gen.chain_dataset("small", num_calls=1, seed=seed + 1, median_n=20000, max_n=20000)
+    k = np.arange(u.nanchors)
+    k[100:110] = k[100:110][::-1]  # x no longer sorted
+    parts.append(gen.ChainCalls(u.offsets, u.x[k], u.y[k], u.avg_qspan, u.params4))
+    return _concat_calls(parts)
+
+
+@pytest.fixture(scope="module")
+def split_calls():
+    calls = split_set(21)
+    return calls, oracle_lib.chain_oracle(calls, 8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split,fault", [("", 0), ("0", 0), ("256,0", 0), ("64,0", 0), ("128,8", 37), ("", 997)])
+def test_gpu_split_exact(split_calls, monkeypatch, split, fault):
+    """Long calls as speculative segments (csrc/chain_split.hip) give the sequential loop's results
+    bit for bit: default and tiny segments, no warm-up, and injected wrong guesses that the
+    verification must catch and the sequential fix-up repair."""
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    calls, exp = split_calls
+    monkeypatch.setenv("GB_CHAIN_SPLIT", split)
+    monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
+    ns, rounds, fixups = b.split_stats()
+    if split == "0":
+        assert ns == 0
+    else:
+        long_sorted = sum(1 for c in range(calls.ncalls) if calls.offsets[c + 1] - calls.offsets[c] >= 2 * (
+            int(split.split(",")[0]) if split else 4096))
+        assert 0 < ns < long_sorted  # the unsorted long call stays whole
+    if fault:
+        assert fixups > 0 and rounds > 1
+    b.run()  # re-run on the same buffers
+    assert_same(b.results(), exp)
+    b.close()

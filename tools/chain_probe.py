@@ -26,8 +26,9 @@ def t(c, reps=3):
     for _ in range(reps):
         b.run(); b.sync(); ms.append(b.timing())
     v = b.results()[4]
+    st = b.split_stats()
     b.close()
-    return min(ms), v
+    return min(ms), v, st
 
 
 lens = calls.offsets[1:] - calls.offsets[:-1]
@@ -35,6 +36,7 @@ order = np.argsort(-lens)
 for name, idx in [("all", np.arange(calls.ncalls)), ("longest", order[:1]), ("top8", order[:8]),
                   ("rest", order[1:]), ("short_half", order[calls.ncalls // 2:])]:
     c = sub(idx)
-    ms, v = t(c)
+    ms, v, st = t(c)
     print(f"{name:10s} calls {c.ncalls:6d} anchors {c.nanchors:9d} visited {v:11d} kernel {ms:8.2f} ms "
-          f"-> {ms * 1e6 / max(lens[idx].max(), 1):.1f} ns per anchor of the longest call", flush=True)
+          f"-> {ms * 1e6 / max(lens[idx].max(), 1):.1f} ns per anchor of the longest call; split calls, rounds, "
+          f"fix-ups {st}", flush=True)
