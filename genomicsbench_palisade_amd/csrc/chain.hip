@@ -69,9 +69,11 @@ __device__ __forceinline__ int32_t lds_count(int *p) {
 // by its seq word at step i+1; the producer polls the consumer's `consumed` count with s_sleep.
 // PROF (GB_CHAIN_PROF): 1 = start/end stamps (100 MHz) of the first/longest call and of the
 // whole grid; 2 = also phase clocks: head, steps, tail, nsteps, slot misses, miss ticks.
-template <int PROF>
+// RING: the stamp ring (kRing for any window, kRingSmall for blocks whose windows are known to hold
+// <= kRingSmall anchors: 12 KB less LDS, three times the blocks per CU).
+template <int PROF, int RING>
 __global__ __launch_bounds__(128) void chain_kernel(Args A) {
-  __shared__ uint32_t S[kRing + 64];
+  __shared__ uint32_t S[RING + 64];
   __shared__ Slot ring[kSlots];
   __shared__ int consumed;
   const VCall &V = A.vc[blockIdx.x];
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
   int32_t *score = (scr ? A.s_score : A.score) + V.out, *parent = (scr ? A.s_parent : A.parent) + V.out;
   int32_t *target = A.target + V.out, *peak = A.peak + V.out;  // written by kVFinal blocks only
 
-  for (int k = threadIdx.x; k < kRing + 64; k += 128) S[k] = 0;
+  for (int k = threadIdx.x; k < RING + 64; k += 128) S[k] = 0;
   if (fin)
     for (int32_t k = threadIdx.x; k < n; k += 128) target[k] = 0;  // a fresh std::vector in the reference
   if (threadIdx.x < kSlots) ring[threadIdx.x].seq = 0;
@@ -260,8 +262,8 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
     if (PROF >= 1 && (A.exp & 8)) {
       pt = 0;
     } else {
-      S[(ok & (lane > 0) & (wp1 >= pst)) ? (wp1 & (kRing - 1)) : kRing + lane] = (uint32_t)(a + 1);
-      pt = (int32_t)S[(a - 1 - lane) & (kRing - 1)];
+      S[(ok & (lane > 0) & (wp1 >= pst)) ? (wp1 & (RING - 1)) : RING + lane] = (uint32_t)(a + 1);
+      pt = (int32_t)S[(a - 1 - lane) & (RING - 1)];
     }
     psg0 = __builtin_amdgcn_readfirstlane(sg);
   };
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
         // this anchor's own stamps first (the next anchor's preparation overwrote them)
         const uint32_t stamp = (uint32_t)(i + 1);
         const bool okl = (okm >> lane) & 1;
-        S[(okl & (pjv >= st)) ? (pjv & (kRing - 1)) : kRing + lane] = stamp;
+        S[(okl & (pjv >= st)) ? (pjv & (RING - 1)) : RING + lane] = stamp;
         // the wave's flushed score/parent stores reach L2 before these sc1 reads of them
         __builtin_amdgcn_s_waitcnt(0);
         const uint64_t xi = X[i], yi = Y[i];
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(128) void chain_kernel(Args A) {
           }
           int32_t sgo;
           const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
-          if (resolve_step(oko ? sgo + scj : INT_MIN, oko, pj, jt, st, stamp, lane, neg_lane, trs, i, S, M, J, N,
+          if (resolve_step<kMarkStore, RING>(oko ? sgo + scj : INT_MIN, oko, pj, jt, st, stamp, lane, neg_lane, trs, i, S, M, J, N,
                            vis_i))
             break;
         }
@@ -488,8 +490,9 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
 }  // namespace
 
 namespace gbchain {
-// One launch of the sequential kernel over nvc blocks of the block table d_vc.
-int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof) {
+// One launch of the sequential kernel over nvc blocks of the block table d_vc, with the small stamp
+// ring (small: every block's windows hold <= kRingSmall anchors) or the full one.
+int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool small, hipStream_t stream) {
   if (nvc <= 0) return GB_OK;
   Args A;
   A.vc = d_vc;
@@ -507,14 +510,40 @@ int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof) {
   A.visited = B->d_vis;
   A.prof = prof ? B->d_prof : nullptr;
   A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
-  if (prof == 2)
-    hipLaunchKernelGGL(chain_kernel<2>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
-  else if (prof == 1)
-    hipLaunchKernelGGL(chain_kernel<1>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
-  else
-    hipLaunchKernelGGL(chain_kernel<0>, dim3((unsigned)nvc), dim3(128), 0, B->stream, A);
+  const dim3 g((unsigned)nvc), b(128);
+  if (small) {
+    if (prof == 2)
+      hipLaunchKernelGGL((chain_kernel<2, kRingSmall>), g, b, 0, stream, A);
+    else if (prof == 1)
+      hipLaunchKernelGGL((chain_kernel<1, kRingSmall>), g, b, 0, stream, A);
+    else
+      hipLaunchKernelGGL((chain_kernel<0, kRingSmall>), g, b, 0, stream, A);
+  } else {
+    if (prof == 2)
+      hipLaunchKernelGGL((chain_kernel<2, kRing>), g, b, 0, stream, A);
+    else if (prof == 1)
+      hipLaunchKernelGGL((chain_kernel<1, kRing>), g, b, 0, stream, A);
+    else
+      hipLaunchKernelGGL((chain_kernel<0, kRing>), g, b, 0, stream, A);
+  }
   GB_HIP(hipGetLastError());
   return GB_OK;
+}
+
+// The block table of a batch: small-ring blocks first (on the batch's stream), full-ring blocks
+// concurrently on the second stream.
+int launch_table(gb_chain_batch *B, int prof) {
+  const int nvc = (int)B->vc.size(), ns = B->n_small;
+  if (ns < nvc && ns > 0) {
+    GB_HIP(hipEventRecord(B->fj[0], B->stream));
+    GB_HIP(hipStreamWaitEvent(B->stream2, B->fj[0], 0));
+    if (int st = launch_chain(B, B->d_vc + ns, nvc - ns, prof, false, B->stream2)) return st;
+    GB_HIP(hipEventRecord(B->fj[1], B->stream2));
+    if (int st = launch_chain(B, B->d_vc, ns, prof, true, B->stream)) return st;
+    GB_HIP(hipStreamWaitEvent(B->stream, B->fj[1], 0));
+    return GB_OK;
+  }
+  return launch_chain(B, B->d_vc, nvc, prof, ns == nvc, B->stream);
 }
 }  // namespace gbchain
 
@@ -523,8 +552,11 @@ int batch_new(gb_chain_batch **out) {
   auto *B = new gb_chain_batch();
   hipError_t e = hipGetDevice(&B->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream2, hipStreamNonBlocking);
   for (auto &ev : B->ev)
     if (e == hipSuccess) e = hipEventCreate(&ev);
+  for (auto &ev : B->fj)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&B->d_vis, sizeof(unsigned long long));
   if (e != hipSuccess) {
     gb::set_error("gb_chain: %s", hipGetErrorString(e));
@@ -574,7 +606,7 @@ int gb_chain_batch_run(gb_chain_batch *B) {
     // split calls: their targets past segment 0 are marked later by atomic max over zeros
     if (!B->split.empty())
       GB_HIP(hipMemsetAsync(B->d_out + 2 * std::max<int64_t>(B->nanchors, 1), 0, (size_t)B->nanchors * 4, B->stream));
-    if (int st = gbchain::launch_chain(B, B->d_vc, (int)B->vc.size(), prof)) return st;
+    if (int st = gbchain::launch_table(B, prof)) return st;
     if (!B->split.empty())
       if (int st = gbchain::split_resolve(B)) return st;
   }
@@ -644,6 +676,9 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
     (void)hipFree(p);
   for (auto ev : B->ev)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : B->fj)
+    if (ev) (void)hipEventDestroy(ev);
+  if (B->stream2) (void)hipStreamDestroy(B->stream2);
   if (B->stream) (void)hipStreamDestroy(B->stream);
   delete B;
   return GB_OK;

@@ -8,7 +8,8 @@
 
 namespace gbchain {
 
-constexpr int kRing = 8192;     // stamp ring >= max_iter (5000) + 64 candidates
+constexpr int kRing = 8192;      // stamp ring >= max_iter (5000) + 64 candidates: any window
+constexpr int kRingSmall = 1024; // for blocks whose windows hold <= 1024 anchors (i - st(i))
 constexpr int kMaxIter = 5000;  // host_kernel.cpp:41
 constexpr int kMaxSkip = 25;    // host_kernel.cpp:42
 
@@ -87,15 +88,16 @@ constexpr int32_t kNoCand = INT_MIN;  // sg of a filtered candidate (producer ->
 // per call), kMarkNone not at all, kMarkMax an atomic max into `tgt` (anchors of one call resolved
 // in parallel: the last marker is the largest i).
 enum { kMarkStore = 0, kMarkNone = 1, kMarkMax = 2 };
-template <int MARK = kMarkStore>
+// RING: stamp ring size; positions of one loop lie in [st, i-1], so i - st <= RING keeps them apart.
+template <int MARK = kMarkStore, int RING = kRing>
 __device__ __forceinline__ bool resolve_step(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, uint32_t stamp,
                                              int lane, int32_t neg_lane, __amdgpu_buffer_rsrc_t trs, int32_t i,
                                              uint32_t *S, int32_t &M, int32_t &J, int32_t &N, uint32_t &vis,
                                              int32_t *tgt_out = nullptr) {
   // "targets[j] == i": stamps from visited j' > j with parents[j'] == j. A stamp can only match a
   // lane whose j >= st (|pj - j| < kRing, so equal ring slots mean pj == j), so no validity test
-  S[(ok & (pj >= st)) ? (pj & (kRing - 1)) : kRing + lane] = stamp;
-  const bool tgt = S[(jtop - lane) & (kRing - 1)] == stamp;
+  S[(ok & (pj >= st)) ? (pj & (RING - 1)) : RING + lane] = stamp;
+  const bool tgt = S[(jtop - lane) & (RING - 1)] == stamp;
   const int32_t mx = scan_max(sc);  // inclusive max scan
   const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
   const bool upd = sc > before;  // false on filtered lanes: before >= M >= 0 > INT_MIN

@@ -45,6 +45,8 @@ struct gb_chain_batch {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  hipStream_t stream2 = nullptr;            // full-ring blocks run here, beside the small-ring ones
+  hipEvent_t fj[2] = {nullptr, nullptr};    // fork / join of the two streams
   int64_t ncalls = 0, nanchors = 0;
   int64_t cap_calls = 0, cap_anchors = 0;  // allocated sizes (a refilled batch reuses its buffers)
   int64_t *d_off = nullptr;
@@ -57,8 +59,10 @@ struct gb_chain_batch {
   bool ran = false;
   gbchain::ChainBt *bt = nullptr;  // backtrack state (gb_chain_batch_backtrack)
 
-  // the block table of the sequential kernel, longest first
+  // the block table of the sequential kernel: n_small small-ring blocks, then the others, each
+  // class longest first
   std::vector<gbchain::VCall> vc;
+  int n_small = 0;
   gbchain::VCall *d_vc = nullptr;
   int64_t cap_vc = 0;
   // long calls as speculative segments (chain_split.hip); empty when no call is split
@@ -87,5 +91,6 @@ namespace gbchain {
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4);
 int split_resolve(gb_chain_batch *B);
 void split_free(gb_chain_batch *B);
-int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof);
+int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool small, hipStream_t stream);
+int launch_table(gb_chain_batch *B, int prof);
 }  // namespace gbchain

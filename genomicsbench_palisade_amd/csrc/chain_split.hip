@@ -32,6 +32,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "../../include/gb_chain.h"
@@ -361,27 +362,57 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   B->st.clear();
   B->scratch_n = 0;
   B->max_split_n = 0;
+  // per call: the widest window (i - st(i), st as the reference's loop walks it,
+  // host_kernel.cpp:57-58) and whether x is sorted; calls in parallel
+  std::vector<int32_t> maxwin((size_t)ncalls, 0);
+  std::vector<uint8_t> sorted((size_t)ncalls, 0);
+  auto walk = [&](int64_t c, int32_t *stw) {
+    const int64_t off = offsets[c];
+    const int32_t n = (int32_t)(offsets[c + 1] - off);
+    const uint64_t mdx = (uint64_t)(int64_t)params4[4 * c];
+    int32_t s = 0, mw = 0;
+    bool srt = true;
+    for (int32_t i = 0; i < n; i++) {
+      while (s < i && x[off + i] > x[off + s] + mdx) ++s;
+      if (i - s > kMaxIter) s = i - kMaxIter;
+      if (stw) stw[i] = s;
+      mw = std::max(mw, i - s);
+      if (i) srt &= x[off + i] >= x[off + i - 1];
+    }
+    maxwin[(size_t)c] = mw;
+    sorted[(size_t)c] = srt;
+  };
+  {
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                 offsets[ncalls] / 200000 + 1}));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&, t] {
+        for (int64_t c = t; c < ncalls; c += nt) walk(c, nullptr);
+      });
+    for (auto &t : th) t.join();
+  }
+  auto vpush = [&](int64_t in, int64_t out, int32_t n, int64_t c, int32_t mode, int32_t win) {
+    B->vc.push_back({in, out, n, (int32_t)c, 0, mode, 0, win <= kRingSmall ? 1 : 0});
+  };
   std::vector<int32_t> stw;
   for (int64_t c = 0; c < ncalls; c++) {
     const int64_t off = offsets[c];
     const int32_t n = (int32_t)(offsets[c + 1] - off);
-    bool split = seg >= 64 && (int64_t)n >= 2 * (int64_t)seg;
-    for (int32_t i = 1; split && i < n; i++) split = x[off + i] >= x[off + i - 1];
+    bool split = seg >= 64 && (int64_t)n >= 2 * (int64_t)seg && sorted[(size_t)c];
     // the chunk space (64 * chunks) is indexed with int32
     if (split && 64 * ((int64_t)B->chunks.size() + n / 64 + 1) >= INT32_MAX) split = false;
     if (!split) {
-      B->vc.push_back({off, off, n, (int32_t)c, 0, kVFinal, 0, 0});
+      vpush(off, off, n, c, kVFinal, maxwin[(size_t)c]);
       continue;
     }
-    // st(i) as the reference's loop walks it (host_kernel.cpp:57-58)
     stw.resize((size_t)n);
-    const uint64_t mdx = (uint64_t)(int64_t)params4[4 * c];
-    int32_t s = 0;
-    for (int32_t i = 0; i < n; i++) {
-      while (s < i && x[off + i] > x[off + s] + mdx) ++s;
-      if (i - s > kMaxIter) s = i - kMaxIter;
-      stw[(size_t)i] = s;
-    }
+    walk(c, stw.data());
+    auto win = [&](int32_t a, int32_t e) {
+      int32_t w = 0;
+      for (int32_t i = a; i < e; i++) w = std::max(w, i - std::max(a, stw[(size_t)i]));
+      return w;
+    };
     SplitCall S;
     S.off = off;
     S.n = n;
@@ -390,7 +421,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     S.nseg = n / seg;
     S.c1 = seg;
     S.cbase = (int32_t)B->chunks.size();
-    B->vc.push_back({off, off, seg, (int32_t)c, 0, kVFinal, 0, 0});  // segment 0: exact
+    vpush(off, off, seg, c, kVFinal, win(0, seg));  // segment 0: exact
     B->segs.push_back({0, seg, 0, 0, -1});
     for (int32_t k = 1; k < S.nseg; k++) {
       Seg G;
@@ -400,7 +431,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
       G.pad = 0;
       G.soff = B->scratch_n;
       B->scratch_n += G.es - G.as;
-      B->vc.push_back({off + G.as, G.soff, G.es - G.as, (int32_t)c, 0, kVScratch, 0, 0});
+      vpush(off + G.as, G.soff, G.es - G.as, c, kVScratch, win(G.as, G.es));
       B->segs.push_back(G);
     }
     const int32_t sc = (int32_t)B->split.size();
@@ -410,8 +441,16 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     B->split.push_back(S);
     B->max_split_n = std::max(B->max_split_n, n);
   }
-  // longest blocks first: the grid is dispatched in order, so the critical paths start first
-  std::stable_sort(B->vc.begin(), B->vc.end(), [](const VCall &a, const VCall &b) { return a.n > b.n; });
+  // small-ring blocks, then the others (VCall::pad holds the class until here); longest first in
+  // each: the grid is dispatched in order, so the critical paths start first
+  std::stable_sort(B->vc.begin(), B->vc.end(), [](const VCall &a, const VCall &b) {
+    return a.pad != b.pad ? a.pad > b.pad : a.n > b.n;
+  });
+  B->n_small = 0;
+  for (auto &v : B->vc) {
+    B->n_small += v.pad;
+    v.pad = 0;
+  }
   const int64_t nvc = (int64_t)B->vc.size();
   // room for one fix-up block per split call behind the table (split_resolve)
   if (int st = grow(&B->d_vc, &B->cap_vc, nvc + (int64_t)B->split.size())) return st;
@@ -490,7 +529,7 @@ int split_resolve(gb_chain_batch *B) {
     // fix-up blocks go behind the block table (split_plan left room for one per split call)
     VCall *d_fix = B->d_vc + B->vc.size();
     GB_HIP(hipMemcpyAsync(d_fix, fix.data(), fix.size() * sizeof(VCall), hipMemcpyHostToDevice, B->stream));
-    if (int st = launch_chain(B, d_fix, (int)fix.size(), 0)) return st;
+    if (int st = launch_chain(B, d_fix, (int)fix.size(), 0, false, B->stream)) return st;
     GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));  // the host vectors are reused next round
   }
