@@ -10,13 +10,16 @@
 // Must be built with -ffp-contract=off: no FMA anywhere, so every cell is bit-identical to the
 // reference's AVX kernels.
 //
-// MI355X design: one testcase per wave64; the read is cut into stripes of 64 rows, lane k owns row
-// r0+k and the wave sweeps anti-diagonals (step t: lane k is at column t-k+1). Values move one lane
+// MI355X design: one stack of testcases sharing a haplotype per wave64 (phmm_stack: reads stacked
+// vertically, each behind two virtual rows that reproduce the initial row); the stack is cut into
+// stripes of 64 rows, lane k owns row r0+k and the wave sweeps anti-diagonals (step t: lane k is at
+// column t-k+1). Values move one lane
 // down per step with DPP wave_shr:1 (no LDS round trip); lane 0 takes the row above the stripe from
 // one uniform LDS record per step, every lane reads the haplotype code of its own column from an
 // LDS byte array, and lane 63 writes the stripe's last row back into the records (in place: the
-// write index trails the read index by 63 columns). The f32 pass appends testcases that need f64 to a device list; a second kernel
-// recomputes them in f64. Testcases are ordered by descending cost so the dispatcher balances waves.
+// write index trails the read index by 63 columns). A second, persistent kernel recomputes in f64
+// the testcases whose f32 result fell below MIN_ACCEPTED, stack by stack. Stacks are ordered by
+// descending cost so the dispatcher balances waves.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,6 +29,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/gb_phmm.h"
@@ -38,7 +42,9 @@ constexpr int kWave = 64;
 // kBndPad + kWave pad columns) must fit the 160 KB of one CU.
 constexpr int kMaxHaplen = 9400;
 constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_stripe reads)
+constexpr int kRecPad = 4;   // boundary records below column 0 (lane 63's writes start at column -2)
 constexpr int kQualTab = 128;
+constexpr int kStackRows = 1024;  // rows per stack (a testcase taller than this gets its own)
 constexpr int kM2M = ((127 * 128) >> 1) + 128;  // set_mm_prob indices for quals < 128
 
 // ---------------------------------------------------------------------------------------------
@@ -187,10 +193,12 @@ __device__ __forceinline__ double select_dist(uint32_t rmask, uint32_t h, double
 
 // Per-lane constants of one stripe (initializeVectors, avx-pairhmm-template.h:83-128): the lane's
 // own row (Y recurrence, emission) and the NEXT row's transitions (the partials z/w it hands down).
+// nGAPMx is nGAPM for the X term of the bracket; a separate register so that the virtual row 0 of
+// a stacked testcase (phmm_stack) can drop the X it receives from the testcase above it.
 template <typename T>
 struct RowParams {
   T pMY, pYY, dmatch, dmis;              // own row
-  T nMM, nGAPM, nMX, nXX;                // row below (lane+1; lane 63: first row of next stripe)
+  T nMM, nGAPM, nGAPMx, nMX, nXX;        // row below (lane+1; lane 63: first row of next stripe)
   uint32_t rmask;
 };
 
@@ -206,7 +214,9 @@ struct LaneState {
 //   X = M[r-1][c]*pMX + X[r-1][c]*pXX         computed by lane-1 as w, shifted in
 //   M = ((M*pMM + X*pGAPM) + Y*pGAPM)[r-1][c-1] * dist    bracket computed by lane-1 as z
 //   Y = M[r][c-1]*pMY + Y[r][c-1]*pYY
-template <typename T, bool kLast>
+// kSum: accumulate the row sums (a testcase's last row is in the stripe); kWrite: lane 63 hands its
+// row's partials to the next stripe through the LDS records.
+template <typename T, bool kSum, bool kWrite>
 __device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneState<T> &st,
                                           const RowParams<T> &P, T &sumM, T &sumX, Brec<T> *wr, bool last_lane) {
   const T X = dpp<dpp_shr>(st.wo, rec.w);          // X[r][c]
@@ -214,12 +224,13 @@ __device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneSt
   const T dist = select_dist(P.rmask, h, P.dmatch, P.dmis);
   const T M = st.zd * dist;
   const T Y = st.Mp * P.pMY + st.Yp * P.pYY;
-  st.zo = (M * P.nMM + X * P.nGAPM) + Y * P.nGAPM;
+  st.zo = (M * P.nMM + X * P.nGAPMx) + Y * P.nGAPM;
   st.wo = M * P.nMX + X * P.nXX;
-  if constexpr (kLast) {
+  if constexpr (kSum) {
     sumM = sumM + M;
     sumX = sumX + X;
-  } else {
+  }
+  if constexpr (kWrite) {
     // lane 63 hands its row's z/w (the next stripe's brackets) to LDS; columns < 1 land in the pad
     if (last_lane) {
       Brec<T> b;
@@ -235,35 +246,65 @@ __device__ __forceinline__ void phmm_step(const Brec<T> &rec, uint32_t h, LaneSt
 
 // Sweep `steps` anti-diagonals of one stripe, 4 per iteration, the boundary records of the next
 // block prefetched before this block runs. Reads are at columns > t; lane 63 writes column t-62 of
-// the row below at step t (bnd has kWave pad records below column 0 for the first 62 steps).
-template <typename T, bool kLast>
+// the row below at step t from step 60 on (bnd has kRecPad pad records below column 0).
+// kSum: the lanes in `lastmask` hold the last row of a testcase; lane k reaches column C at step
+// C + k - 1, where its row sum is final, so that step runs singly and lane k stores sumM + sumX
+// (later steps add columns beyond C). The check is a uniform scalar compare per 4 steps.
+template <typename T, bool kSum, bool kWrite>
 __device__ __forceinline__ void phmm_stripe(int steps, LaneState<T> &st, const RowParams<T> &P,
                                             T &sumM, T &sumX, Brec<T> *__restrict__ bnd,
-                                            const uint8_t *__restrict__ hcol, int C, int lane) {
+                                            const uint8_t *__restrict__ hcol, int C, int lane,
+                                            uint64_t lastmask, T *__restrict__ out) {
   // hcol[c] = haplotype code of column c (valid for c in [-63, C+kBndPad)); lane's column at step
   // t is t - lane + 1.
   const uint8_t *hl = hcol + 1 - lane;
   const bool last_lane = lane == kWave - 1;
   constexpr int U = 4;
-  int t = 0;
+  // lane 63 reaches column 0 at step 62: its records for earlier (negative) columns are dropped by
+  // running the first 60 steps without writes (the pad holds columns -2, -1)
+  constexpr int kNoWrite = 60;
+  uint64_t pend = lastmask;
+  int target = (kSum && pend) ? C + __builtin_ctzll(pend) - 1 : INT_MAX;
+  auto single = [&](int tt, auto wr_tag) {
+    constexpr bool W = decltype(wr_tag)::value;
+    phmm_step<T, kSum, W>(bnd[tt + 1], hl[tt], st, P, sumM, sumX, bnd + (tt - (kWave - 2)), last_lane);
+    if (kSum && tt == target) {
+      if (lane == __builtin_ctzll(pend)) *out = sumM + sumX;
+      pend &= pend - 1;
+      target = pend ? C + __builtin_ctzll(pend) - 1 : INT_MAX;
+    }
+  };
   // The block's record reads and writes go through one VGPR address with immediate offsets (an
   // SGPR base costs a v_mov per access); the asm zero keeps the compiler from rematerialising it.
   int vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   Brec<T> *wb = bnd - (kWave - 2) + vzero;
-  for (; t + U <= steps; t += U) {
-    // records land directly in the DPP "old" registers (no rotation copies); the LDS latency is
-    // covered by the other waves on the SIMD
-    Brec<T> *wr = wb + t;
-    const Brec<T> c0 = wr[kWave - 1], c1 = wr[kWave], c2 = wr[kWave + 1], c3 = wr[kWave + 2];
-    const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
-    phmm_step<T, kLast>(c0, h0, st, P, sumM, sumX, wr, last_lane);
-    phmm_step<T, kLast>(c1, h1, st, P, sumM, sumX, wr + 1, last_lane);
-    phmm_step<T, kLast>(c2, h2, st, P, sumM, sumX, wr + 2, last_lane);
-    phmm_step<T, kLast>(c3, h3, st, P, sumM, sumX, wr + 3, last_lane);
+  auto run = [&](int t, int end, auto wr_tag) {
+    constexpr bool W = decltype(wr_tag)::value;
+    for (; t + U <= end; t += U) {
+      if (kSum && target < t + U) {
+        for (int u = 0; u < U; u++) single(t + u, wr_tag);
+        continue;
+      }
+      // records land directly in the DPP "old" registers (no rotation copies); the LDS latency is
+      // covered by the other waves on the SIMD
+      Brec<T> *wr = wb + t;
+      const Brec<T> c0 = wr[kWave - 1], c1 = wr[kWave], c2 = wr[kWave + 1], c3 = wr[kWave + 2];
+      const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
+      phmm_step<T, kSum, W>(c0, h0, st, P, sumM, sumX, wr, last_lane);
+      phmm_step<T, kSum, W>(c1, h1, st, P, sumM, sumX, wr + 1, last_lane);
+      phmm_step<T, kSum, W>(c2, h2, st, P, sumM, sumX, wr + 2, last_lane);
+      phmm_step<T, kSum, W>(c3, h3, st, P, sumM, sumX, wr + 3, last_lane);
+    }
+    for (; t < end; t++) single(t, wr_tag);
+  };
+  if constexpr (kWrite) {
+    const int a = min(steps, kNoWrite);
+    run(0, a, std::false_type{});
+    run(a, steps, std::true_type{});
+  } else {
+    run(0, steps, std::false_type{});
   }
-  for (; t < steps; t++)
-    phmm_step<T, kLast>(bnd[t + 1], hl[t], st, P, sumM, sumX, bnd + (t - (kWave - 2)), last_lane);
 }
 
 template <typename T>
@@ -284,112 +325,195 @@ __device__ __forceinline__ void load_row(const uint8_t *__restrict__ rbase, int 
   dmis = tab.div3[q];
 }
 
-// One testcase per 64-lane workgroup (f32 pass: blockIdx = testcase; f64 pass over every testcase
-// when `f64_list` is null). The f64 fallback pass is persistent instead: a grid sized to the
-// resident capacity takes the testcases the f32 pass flagged from `f64_list` through the counter
-// f64_count[1], so no workgroup is launched for the ~70 % of testcases that need no fallback.
-template <typename T, bool kF64Pass>
-__device__ __forceinline__ void phmm_testcase(int w, const TcDesc *__restrict__ descs,
-                                              const uint8_t *__restrict__ pool, const DevTab<T> &tab,
-                                              T *__restrict__ raw_out, int *__restrict__ f64_list,
-                                              int *__restrict__ f64_count, uint8_t *smem_raw);
+// Stacks: testcases that share a haplotype are stacked into one tall matrix, so a wave sweeps
+// 64-row stripes of the stack and a read's rows need not start at a stripe boundary: the partial
+// last stripe of every testcase (a quarter of all lane steps for 100-250-row reads) disappears.
+// Each read is preceded by two virtual rows, ordinary lanes whose constants make the shared step
+// code produce the reference's initial row (M = X = 0, Y = INITIAL_CONSTANT / haplen) exactly, and
+// zeros at the columns a lane sweeps before its column 1 (so nothing leaks into column 0):
+//   va: dist = 0 (M = 0), Y = init_Y * 1 at every step, partials z = (0*0 + X*0) + init_Y*1 and
+//       w = 0*0 + X*0 = 0, whatever the testcase above hands it;
+//   v0: dist = 1 at columns >= 0 and 0 before (column codes 5 at column 0, 6 below it, matched by
+//       v0's mask only up to 5), so M = init_Y from column 0 on, and its partials are
+//       z = (M*pGAPM + X*0) + 0*0 = init_Y*pGAPM (the reference's (0*pMM + 0*pGAPM) + init_Y*pGAPM)
+//       and w = 0 (its 0*pMX + 0*pXX), zero before column 0.
+// Lanes beyond the stack's last row compute zeros.
+struct __attribute__((aligned(16))) Stack {
+  uint32_t first;  // first entry in the stack's testcase index list
+  uint32_t count;  // testcases (<= 64)
+  uint32_t hap_off;
+  uint32_t C;
+};
+struct __attribute__((aligned(16))) StackEnt {
+  int start;  // stacked row of the testcase's first virtual row
+  int R;
+  uint32_t read_off, out_idx;
+};
 
-template <typename T, bool kF64Pass>
-__global__ __launch_bounds__(64) void phmm_forward(const TcDesc *__restrict__ descs,
-                                                    const uint8_t *__restrict__ pool,
-                                                    DevTab<T> tab, T *__restrict__ raw_out,
-                                                    int *__restrict__ f64_list,
-                                                    int *__restrict__ f64_count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  if constexpr (kF64Pass) {
-    if (f64_list) {
-      const int total = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f64_count, __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT));
-      while (true) {
-        int k = 0;
-        if (threadIdx.x == 0) k = atomicAdd(f64_count + 1, 1);
-        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-        if (k >= total) return;
-        phmm_testcase<T, true>(f64_list[k], descs, pool, tab, raw_out, nullptr, nullptr, smem_raw);
-        __syncthreads();  // the next testcase re-initialises the LDS records
-      }
-    }
-  }
-  phmm_testcase<T, kF64Pass>(blockIdx.x, descs, pool, tab, raw_out, f64_list, f64_count, smem_raw);
+__device__ __forceinline__ int scan_add(int v) {  // wave-wide inclusive prefix sum (DPP)
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  return v;
 }
 
+// One stack. f32 pass: every testcase; f64 pass: those whose f32 result is below MIN_ACCEPTED
+// (all of them when `force`). Returns the number of testcases computed.
 template <typename T, bool kF64Pass>
-__device__ __forceinline__ void phmm_testcase(int w, const TcDesc *__restrict__ descs,
-                                              const uint8_t *__restrict__ pool, const DevTab<T> &tab,
-                                              T *__restrict__ raw_out, int *__restrict__ f64_list,
-                                              int *__restrict__ f64_count, uint8_t *smem_raw) {
-  const TcDesc desc = descs[w];
-  const int R = (int)(desc.dims & 0xffff);
-  const int C = (int)(desc.dims >> 16);
+__device__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
+                          const uint8_t *__restrict__ pool, const DevTab<T> &tab, T *__restrict__ raw_out,
+                          const float *__restrict__ raw_f, bool force, uint8_t *smem_raw) {
   const int lane = threadIdx.x;
-  const T init_Y = tab.init_const / (T)C;
-  const uint8_t *rbase = pool + desc.read_off;
-  // LDS: boundary records for columns [0, C+kBndPad), then haplotype codes for columns
-  // [-kWave, C+kBndPad) (codes 0 outside 1..C; cells outside the matrix never feed real cells).
-  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw) + kWave;  // kWave pad records below column 0
-  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad + kWave) + kWave;
+  const int C = (int)S.C;
+  // LDS: boundary records for columns [-kRecPad, C+kBndPad) and the haplotype codes for columns
+  // [-kWave, C+kBndPad). The stack's testcase table lives in lanes (lane a: entry a), read with
+  // cross-lane shuffles.
+  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw) + kRecPad;
+  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad + kRecPad) + kWave;
 
-  // Row 0 -> first row's partials: M = X = 0, Y = init_Y, so z = (0*pMM + 0*pGAPM) + init_Y*pGAPM
-  // (evaluated, not simplified, to keep the reference's operation order) and w = 0*pMX + 0*pXX.
-  T z0, w0;
-  {
-    T pMM, pGAPM, pMX, pXX, pMY, pYY, dm, dx;
-    uint32_t rm;
-    load_row(rbase, R, 0, tab, pMM, pGAPM, pMX, pXX, pMY, pYY, dm, dx, rm);
-    const T zero = (T)0;
-    z0 = (zero * pMM + zero * pGAPM) + init_Y * pGAPM;
-    w0 = zero * pMX + zero * pXX;
+  // the stack's testcases, compacted to those computed in this pass
+  TcDesc d = {0, 0, 0, 0};
+  bool act = lane < (int)S.count;
+  if (act) {
+    d = descs[stk_tc[S.first + lane]];
+    if constexpr (kF64Pass) act = force || raw_f[d.out_idx] < 1e-28f;  // MIN_ACCEPTED, pairhmm_common.h:16
   }
-  const uint8_t *hcode = pool + desc.hap_off;
+  const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+  if (!am) return 0;
+  const int na = __builtin_popcountll(am);
+  const int rows = act ? (int)(d.dims & 0xffff) + 2 : 0;
+  const int incl = scan_add(rows);
+  const int T_rows = __builtin_amdgcn_readlane(incl, 63);
+  // compaction: entry a = the a-th computed testcase (lane order), gathered into lane a
+  int src = 0;
+  {
+    uint64_t m = am;
+    for (int a = 0; a < lane && m; a++) m &= m - 1;  // drop the first `lane` active lanes
+    src = m ? __builtin_ctzll(m) : 63;
+  }
+  const int e_start = __shfl(incl - rows, src), e_R = __shfl(rows - 2, src);
+  const uint32_t e_read = (uint32_t)__shfl((int)d.read_off, src), e_out = (uint32_t)__shfl((int)d.out_idx, src);
+  const T init_Y = tab.init_const / (T)C;
+  const uint8_t *hcode = pool + S.hap_off;
   for (int c = lane; c < C + kBndPad; c += kWave) {
     Brec<T> b;
-    b.z = z0;
-    b.w = w0;
+    b.z = (T)0;
+    b.w = (T)0;
     bnd[c] = b;
   }
-  for (int c = lane - kWave; c < C + kBndPad; c += kWave) hcol[c] = (c >= 1 && c <= C) ? hcode[c - 1] : 0;
+  // column codes: the haplotype's at 1..C, 5 at column 0 and 6 below it (see va / v0), 0 beyond C
+  for (int c = lane - kWave; c < C + kBndPad; c += kWave)
+    hcol[c] = (c >= 1 && c <= C) ? hcode[c - 1] : (c == 0 ? 5 : (c < 0 ? 6 : 0));
   __syncthreads();
 
-  const int nstripes = (R + kWave - 1) / kWave;
-  T result = (T)0;
+  const int nstripes = (T_rows + kWave - 1) / kWave;
   for (int s = 0; s < nstripes; s++) {
-    const int r0 = s * kWave;
-    const int nrows = min(kWave, R - r0);
-    RowParams<T> P;
-    {
-      T pMM, pGAPM, pMX, pXX;
-      load_row(rbase, R, min(r0 + lane, R - 1), tab, pMM, pGAPM, pMX, pXX, P.pMY, P.pYY, P.dmatch,
-               P.dmis, P.rmask);
-      T a, b, d, e;
-      uint32_t f;
-      load_row(rbase, R, min(r0 + lane + 1, R - 1), tab, P.nMM, P.nGAPM, P.nMX, P.nXX, a, b, d, e, f);
+    const int g = s * kWave + lane;
+    // the lane's testcase: the last entry starting at or before row g
+    int lo = 0, hi = na - 1;
+    while (__builtin_amdgcn_ballot_w64(lo < hi)) {  // per-lane binary search over lanes' starts
+      const int mid = (lo + hi + 1) >> 1;
+      const int sm = __shfl(e_start, mid);
+      if (lo < hi) {
+        if (sm <= g) lo = mid; else hi = mid - 1;
+      }
     }
+    StackEnt e;
+    e.start = __shfl(e_start, lo);
+    e.R = __shfl(e_R, lo);
+    e.read_off = (uint32_t)__shfl((int)e_read, lo);
+    e.out_idx = (uint32_t)__shfl((int)e_out, lo);
+    const int r = g - e.start;  // 0: va, 1: v0, 2..R+1: read row r-2
+    const bool dead = g >= T_rows;
+    const uint8_t *rbase = pool + e.read_off;
+    RowParams<T> P;
     LaneState<T> st;
-    st.Mp = st.Yp = st.zo = st.wo = (T)0;
-    st.zd = (lane == 0) ? bnd[0].z : (T)0;  // bracket at column 0: z0 for stripe 0, 0 below
+    st.Mp = st.zo = st.wo = (T)0;
+    st.Yp = (T)0;
+    // bracket at column 0 of the row above: lane 0 takes it from the record lane 63 wrote there
+    st.zd = lane == 0 ? bnd[0].z : (T)0;
+    {
+      T pMM, pGAPM, pMX, pXX, a, b, dm, dx;
+      uint32_t f;
+      const T zero = (T)0, one = (T)1;
+      P.nMM = P.nGAPM = P.nGAPMx = P.nMX = P.nXX = zero;
+      if (dead) {
+        P.pMY = P.pYY = P.dmatch = P.dmis = zero;
+        P.rmask = 0;
+      } else if (r == 0) {  // va
+        P.pMY = zero;
+        P.pYY = one;
+        P.dmatch = P.dmis = zero;
+        P.rmask = 0;
+        P.nGAPM = one;
+        st.Yp = init_Y;
+        // the state of a lane that has swept the columns before its first one: va's outputs are
+        // constant, so it hands init_Y down from its first step
+        st.zo = (zero * zero + zero * zero) + init_Y * one;
+      } else if (r == 1) {  // v0
+        P.pMY = P.pYY = zero;
+        P.dmatch = one;
+        P.dmis = zero;
+        P.rmask = 0x3F;
+        load_row(rbase, e.R, 0, tab, pMM, pGAPM, pMX, pXX, a, b, dm, dx, f);
+        P.nMM = pGAPM;
+        st.zd = init_Y;  // va's output at the column before
+        // lane 0 starts at column 1: the row below takes v0's column-0 bracket from its initial zo
+        if (lane == 0) st.zo = (init_Y * P.nMM + zero * zero) + zero * zero;
+      } else {
+        load_row(rbase, e.R, r - 2, tab, pMM, pGAPM, pMX, pXX, P.pMY, P.pYY, P.dmatch, P.dmis, P.rmask);
+        if (r - 1 < e.R) {
+          load_row(rbase, e.R, r - 1, tab, P.nMM, P.nGAPM, P.nMX, P.nXX, a, b, dm, dx, f);
+          P.nGAPMx = P.nGAPM;
+        }  // the last row: nothing below it in this testcase (zero partials)
+      }
+    }
+    const bool last_row = !dead && r == e.R + 1;
+    const uint64_t lastmask = __builtin_amdgcn_ballot_w64(last_row);
+    const bool more = s < nstripes - 1;
+    const int steps = more ? C + kWave - 1 : C + (T_rows - s * kWave) - 1;
     T sumM = (T)0, sumX = (T)0;
-    if (s == nstripes - 1) {
-      phmm_stripe<T, true>(C + nrows - 1, st, P, sumM, sumX, bnd, hcol, C, lane);
-      result = sumM + sumX;
+    T *out = raw_out + e.out_idx;
+    if (lastmask) {
+      if (more)
+        phmm_stripe<T, true, true>(steps, st, P, sumM, sumX, bnd, hcol, C, lane, lastmask, out);
+      else
+        phmm_stripe<T, true, false>(steps, st, P, sumM, sumX, bnd, hcol, C, lane, lastmask, out);
     } else {
-      phmm_stripe<T, false>(C + kWave - 1, st, P, sumM, sumX, bnd, hcol, C, lane);
-      if (lane == 0) bnd[0].z = (T)0;  // rows >= 1 have M = X = Y = 0 at column 0
+      phmm_stripe<T, false, true>(steps, st, P, sumM, sumX, bnd, hcol, C, lane, 0, out);
     }
     __syncthreads();
   }
-  if (lane == ((R - 1) & (kWave - 1))) {
-    raw_out[desc.out_idx] = result;
-    if constexpr (!kF64Pass) {
-      if (result < 1e-28f) {  // MIN_ACCEPTED, pairhmm_common.h:16
-        int slot = atomicAdd(f64_count, 1);
-        f64_list[slot] = w;
-      }
+  return na;
+}
+
+// f32 pass: one stack per workgroup (LPT order). f64 pass: a persistent grid takes stacks through
+// counter[1] and recomputes their testcases whose f32 result fell below MIN_ACCEPTED; counter[0]
+// counts them.
+template <typename T, bool kF64Pass>
+__global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ stacks, int nstacks,
+                                                    const uint32_t *__restrict__ stk_tc,
+                                                    const TcDesc *__restrict__ descs,
+                                                    const uint8_t *__restrict__ pool, DevTab<T> tab,
+                                                    T *__restrict__ raw_out, const float *__restrict__ raw_f,
+                                                    int *__restrict__ counter, int force) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  if constexpr (kF64Pass) {
+    int done = 0;
+    while (true) {
+      int k = 0;
+      if (threadIdx.x == 0) k = atomicAdd(counter + 1, 1);
+      k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+      if (k >= nstacks) break;
+      done += phmm_stack<T, true>(stacks[k], stk_tc, descs, pool, tab, raw_out, raw_f, force != 0, smem_raw);
+      __syncthreads();  // the next stack re-initialises the LDS
     }
+    if (threadIdx.x == 0 && done) atomicAdd(counter, done);
+  } else {
+    phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, smem_raw);
   }
 }
 
@@ -518,8 +642,10 @@ struct gb_phmm_batch {
   float *d_rf = nullptr;
   double *d_rd = nullptr;
   double *d_out = nullptr;
-  int *d_list = nullptr;
-  int *d_count = nullptr;  // [0] f64 fallbacks flagged by the f32 pass, [1] f64 work counter
+  uint32_t *d_stk_tc = nullptr;  // testcase indices, stack by stack
+  Stack *d_stacks = nullptr;     // LPT order
+  int nstacks = 0;
+  int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
   bool ran = false;
@@ -546,7 +672,6 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   std::unordered_map<ReadKey, uint32_t, KeyHash> read_at;
   std::unordered_map<HapKey, uint32_t, KeyHash> hap_at;
   std::vector<TcDesc> desc(n);
-  std::vector<uint64_t> cost(n);
   int max_h = 0;
   int64_t cells = 0;
   for (int k = 0; k < n; k++) {
@@ -589,33 +714,57 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     desc[k].hap_off = hoff;
     desc[k].dims = (uint32_t)t.rslen | ((uint32_t)t.haplen << 16);
     desc[k].out_idx = (uint32_t)k;
-    cost[k] = (uint64_t)((t.rslen + kWave - 1) / kWave) * (uint64_t)(t.haplen + kWave);
     max_h = std::max(max_h, t.haplen);
     cells += (int64_t)t.rslen * t.haplen;
   }
-  // Longest-processing-time-first order (the dispatcher hands out workgroups in grid order).
+  // Stacks (phmm_stack): testcases grouped by haplotype, stacked up to kStackRows rows (R + 2 per
+  // testcase) and 64 testcases; longest-processing-time first (the dispatcher hands out workgroups
+  // in grid order).
   std::vector<int> order(n);
   for (int k = 0; k < n; k++) order[k] = k;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-  std::vector<TcDesc> sorted(n);
-  for (int k = 0; k < n; k++) sorted[k] = desc[order[k]];
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return desc[a].hap_off < desc[b].hap_off; });
+  std::vector<Stack> stacks;
+  std::vector<uint64_t> scost;
+  for (int k = 0; k < n;) {
+    const uint32_t h = desc[order[k]].hap_off;
+    const int C = (int)(desc[order[k]].dims >> 16);
+    Stack S{(uint32_t)k, 0, h, (uint32_t)C};
+    int rows = 0;
+    while (k < n && desc[order[k]].hap_off == h && S.count < (uint32_t)kWave &&
+           (S.count == 0 || rows + (int)(desc[order[k]].dims & 0xffff) + 2 <= kStackRows)) {
+      rows += (int)(desc[order[k]].dims & 0xffff) + 2;
+      S.count++;
+      k++;
+    }
+    stacks.push_back(S);
+    scost.push_back((uint64_t)((rows + kWave - 1) / kWave) * (uint64_t)(C + kWave));
+  }
+  std::vector<int> sorder(stacks.size());
+  for (size_t k = 0; k < stacks.size(); k++) sorder[k] = (int)k;
+  std::stable_sort(sorder.begin(), sorder.end(), [&](int a, int b) { return scost[a] > scost[b]; });
+  std::vector<Stack> sorted_stacks(stacks.size());
+  for (size_t k = 0; k < stacks.size(); k++) sorted_stacks[k] = stacks[sorder[k]];
+  std::vector<uint32_t> stk_tc(order.begin(), order.end());
   if (pool.empty()) pool.resize(4);
   pool.resize((pool.size() + 15) & ~size_t(15));
 
   const size_t nn = std::max(n, 1);
   if (nn > b->cap_n) {
-    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_list})
+    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
+                    (void *)b->d_stacks})
       (void)hipFree(p);
     b->d_desc = nullptr;
     b->d_rf = nullptr;
     b->d_rd = b->d_out = nullptr;
-    b->d_list = nullptr;
+    b->d_stk_tc = nullptr;
+    b->d_stacks = nullptr;
     b->cap_n = 0;
     GB_HIP(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
     GB_HIP(hipMalloc(&b->d_rf, sizeof(float) * nn));
     GB_HIP(hipMalloc(&b->d_rd, sizeof(double) * nn));
     GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
-    GB_HIP(hipMalloc(&b->d_list, sizeof(int) * nn));
+    GB_HIP(hipMalloc(&b->d_stk_tc, sizeof(uint32_t) * nn));
+    GB_HIP(hipMalloc(&b->d_stacks, sizeof(Stack) * nn));  // at most one stack per testcase
     b->cap_n = nn;
   }
   if (pool.size() > b->cap_pool) {
@@ -626,10 +775,16 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     b->cap_pool = pool.size();
   }
   if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 2 * sizeof(int)));
-  if (n) GB_HIP(hipMemcpyAsync(b->d_desc, sorted.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
+  if (n) {
+    GB_HIP(hipMemcpyAsync(b->d_desc, desc.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
+    GB_HIP(hipMemcpyAsync(b->d_stk_tc, stk_tc.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
+    GB_HIP(hipMemcpyAsync(b->d_stacks, sorted_stacks.data(), sizeof(Stack) * sorted_stacks.size(),
+                          hipMemcpyHostToDevice, b->stream));
+  }
   GB_HIP(hipMemcpyAsync(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice, b->stream));
   GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
   b->n = n;
+  b->nstacks = (int)sorted_stacks.size();
   b->max_haplen = max_h;
   b->cells = cells;
   b->ran = false;
@@ -701,22 +856,24 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipMemsetAsync(b->d_count, 0, 2 * sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
-    const size_t span = (size_t)(b->max_haplen + kBndPad + kWave);  // records and code bytes
-    const size_t lds_f = (sizeof(Brec<float>) + 1) * span + 16;
-    const size_t lds_d = (sizeof(Brec<double>) + 1) * span + 16;
+    const size_t rec = (size_t)(b->max_haplen + kBndPad + kRecPad), codes = (size_t)(b->max_haplen + kBndPad + kWave);
+    const size_t lds_f = sizeof(Brec<float>) * rec + codes + 16;
+    const size_t lds_d = sizeof(Brec<double>) * rec + codes + 16;
     auto f32k = phmm_forward<float, false>;
     auto f64k = phmm_forward<double, true>;
+    const int ns = b->nstacks;
     if (!b->force_f64) {
-      hipLaunchKernelGGL(f32k, dim3(n), dim3(kWave), lds_f, b->stream, b->d_desc, b->d_pool,
-                         dev_tab<float>(t->f, t->hf.init_const), b->d_rf, b->d_list, b->d_count);
+      hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
+                         b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
+                         b->d_count, 0);
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
-    // f64 fallback: persistent grid over the flagged list (every testcase when forced)
-    const int g64 = b->force_f64 ? n : std::min(n, b->f64_grid);
-    hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_desc, b->d_pool,
-                       dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
-                       b->force_f64 ? nullptr : b->d_list, b->force_f64 ? nullptr : b->d_count);
+    // f64 fallback: persistent grid over the stacks, each recomputing its flagged testcases
+    const int g64 = std::min(ns, b->f64_grid);
+    hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
+                       b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
+                       b->d_count, b->force_f64 ? 1 : 0);
     GB_HIP(hipGetLastError());
     GB_HIP(hipEventRecord(b->ev[2], b->stream));
     hipLaunchKernelGGL(phmm_finalize, dim3((n + 255) / 256), dim3(256), 0, b->stream, b->d_rf,
@@ -802,7 +959,8 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   (void)hipFree(b->d_rf);
   (void)hipFree(b->d_rd);
   (void)hipFree(b->d_out);
-  (void)hipFree(b->d_list);
+  (void)hipFree(b->d_stk_tc);
+  (void)hipFree(b->d_stacks);
   (void)hipFree(b->d_count);
   for (auto e : b->ev)
     if (e) (void)hipEventDestroy(e);

@@ -145,3 +145,32 @@ def test_phmm_cli(tmp_path):
     assert len(vals) == len(expect)
     assert np.allclose(vals, expect, atol=1e-6, rtol=0)  # "%lf" prints 6 decimals
     assert "PairHMM completed. Kernel runtime:" in out
+
+
+ACGTN = np.frombuffer(b"ACGTN", np.uint8)
+
+
+def _read(rng, rl):
+    b = ACGTN[rng.integers(0, 5, rl)].tobytes()
+    q = rng.integers(6, 41, rl).astype(np.uint8).tobytes()
+    i = rng.integers(40, 46, rl).astype(np.uint8).tobytes()
+    d = rng.integers(40, 46, rl).astype(np.uint8).tobytes()
+    c = np.full(rl, 10, np.uint8).tobytes()
+    return (b, q, i, d, c)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_stack_edges_vs_oracle(phmm, seed):
+    """Stacked testcases (csrc/phmm.hip phmm_stack): reads of 1, 2, 62-66, 127-129 rows and one taller
+    than a stack (> 1024 rows), haplotypes of 1, 3, 63, 64 and 700 columns, many reads per haplotype
+    (stacks of up to 64 testcases whose rows start anywhere in a stripe): bit-exact against the
+    oracle, f32 and f64 results and the fallback choice."""
+    rng = np.random.default_rng(seed)
+    lens = [1, 2, 62, 63, 64, 65, 66, 127, 128, 129, 1100] + list(rng.integers(1, 200, 80))
+    reads = [_read(rng, int(n)) for n in lens]
+    haps = [gen.BASES[rng.integers(0, 4, n)].tobytes() for n in (1, 3, 63, 64, 700, 250)]
+    ta = TestcaseArray(reads, haps)  # the cross product: 91 reads per haplotype
+    got = phmm.compute_likelihoods_both(ta)
+    exp = oracle_run(ta)
+    assert_exact(got, exp)
+    assert (got[3].astype(bool) == exp[3].astype(bool)).all()
