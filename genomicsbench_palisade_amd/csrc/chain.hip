@@ -603,9 +603,6 @@ int gb_chain_batch_run(gb_chain_batch *B) {
       GB_HIP(hipMemsetAsync(B->d_prof, 0, 16 * sizeof(unsigned long long), B->stream));
       GB_HIP(hipMemsetAsync(B->d_prof + 8, 0xff, sizeof(unsigned long long), B->stream));
     }
-    // split calls: their targets past segment 0 are marked later by atomic max over zeros
-    if (!B->split.empty())
-      GB_HIP(hipMemsetAsync(B->d_out + 2 * std::max<int64_t>(B->nanchors, 1), 0, (size_t)B->nanchors * 4, B->stream));
     if (int st = gbchain::launch_table(B, prof)) return st;
     if (!B->split.empty())
       if (int st = gbchain::split_resolve(B)) return st;

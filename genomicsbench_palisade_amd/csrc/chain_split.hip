@@ -60,6 +60,8 @@ struct SplitArgs {
   int32_t *score, *parent, *target, *peak;
   const int32_t *s_score, *s_parent;
   unsigned long long *visited;
+  int32_t *t2;                   // the split anchors' targets marks (atomic max), merged at the end
+  unsigned long long *viscall;   // visited pairs per split call
   int32_t fault;  // GB_CHAIN_SPLIT_FAULT (tests): guesses of every fault-th anchor are made wrong
 };
 
@@ -152,7 +154,6 @@ __device__ __forceinline__ uint32_t ring_tag(int k, int32_t pos) {
   return (uint32_t)(k + 1) | ((uint32_t)pos >> 10 << 7);
 }
 
-template <int MARK>
 __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, int k,
                                                int lane, int32_t neg_lane, uint32_t *S, int32_t &M, int32_t &J,
                                                int32_t &N, uint32_t &vis, bool &conflict, int32_t *tgt, int32_t i) {
@@ -186,23 +187,23 @@ __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, 
   const int32_t m_lu = __builtin_amdgcn_readlane(mx, lu);
   J = um ? jtop - lu : J;
   M = um ? m_lu : M;
-  if (MARK && ok && ((below >> lane) & 1) && pj >= 0) atomicMax(tgt + pj, i);
+  if (ok && ((below >> lane) & 1) && pj >= 0) atomicMax(tgt + pj, i);
   N = __builtin_amdgcn_readlane(n_after, 63);
   return bm != 0;
 }
 
-// 2. verify (MARK 0): re-run the loop of every split anchor i >= front against the guessed window;
-// fail[sc] = the first i whose loop does not give its own guess. MARK 1 (after convergence): the
-// same loops over all split anchors write the targets marks, count the visited pairs and store the
-// peaks resolved in `pv`.
-template <int MARK>
-__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const int32_t *pv) {
+// 2. verify (CHECK): re-run the loop of every split anchor i >= front against the guessed window;
+// fail[sc] = the first i whose loop does not give its own guess. The loops also write their
+// targets marks into t2 and count visited pairs per call: a call that passes in the first round has
+// all of them right; one that ever failed is re-marked after convergence (CHECK false, front = c1).
+template <bool CHECK>
+__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
   __shared__ uint32_t S[kTagRing + 64];
   const Chunk ch = A.chunks[blockIdx.x];
   const SplitCall Sc = A.split[ch.sc];
   const int lane = threadIdx.x;
   const int32_t start = ch.start, n = Sc.n;
-  const int32_t front = MARK ? Sc.c1 : A.front[ch.sc];
+  const int32_t front = A.front[ch.sc];
   const int32_t cnt = min(64, n - start);
   if (start + cnt <= front) return;
   const int c = Sc.call;
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const int32_t *
   const double avg_qspan = (double)A.avg_qspan[c];
   const uint64_t *X = A.x + Sc.off, *Y = A.y + Sc.off;
   const int32_t *score = A.score + Sc.off, *parent = A.parent + Sc.off;
-  int32_t *tgt = A.target + Sc.off;
+  int32_t *tgt = A.t2 + Sc.off;
   for (int t = lane; t < kTagRing + 64; t += 64) S[t] = 0;
   // window: lane l = anchor start-1-l; the chunk's anchors: lane l = start+l
   const int32_t j0 = start - 1 - lane;
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const int32_t *
       const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
       int32_t M = (int32_t)(yi >> 32 & 0xff), J = -1, N = 0;
       bool conflict = false;
-      bool broke = resolve_tagged<MARK>(ok ? sg + wf : INT_MIN, ok, wp, i - 1, st, k, lane, neg_lane, S, M, J, N,
+      bool broke = resolve_tagged(ok ? sg + wf : INT_MIN, ok, wp, i - 1, st, k, lane, neg_lane, S, M, J, N,
                                         vis, conflict, tgt, i);
       for (int32_t jt = i - 65; !broke && jt >= st; jt -= 64) {  // older candidates from memory
         const int32_t jj = jt - lane;
@@ -254,23 +255,38 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const int32_t *
         }
         int32_t sgo;
         const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
-        broke = resolve_tagged<MARK>(oko ? sgo + fj : INT_MIN, oko, pj, jt, st, k, lane, neg_lane, S, M, J, N, vis,
+        broke = resolve_tagged(oko ? sgo + fj : INT_MIN, oko, pj, jt, st, k, lane, neg_lane, S, M, J, N, vis,
                                      conflict, tgt, i);
       }
       const bool clash = __builtin_amdgcn_ballot_w64(conflict) != 0;
-      if (!MARK && (M != fi || J != pi || clash) && first_bad == INT_MAX) first_bad = i;
+      if (CHECK && (M != fi || J != pi || clash) && first_bad == INT_MAX) first_bad = i;
     }
     wx = dpp_shr_u64(wx, xi);
     wy = dpp_shr_u64(wy, yi);
     wf = dpp_shr_i32(wf, fi);
     wp = dpp_shr_i32(wp, pi);
   }
-  if (!MARK) {
-    if (lane == 0 && first_bad != INT_MAX) atomicMin(A.fail + ch.sc, first_bad);
-  } else {
-    if (lane < cnt) A.peak[Sc.off + start + lane] = pv[64 * blockIdx.x + lane];
-    if (lane == 0) atomicAdd(A.visited, (unsigned long long)vis);
+  if (lane == 0) {
+    if (CHECK && first_bad != INT_MAX) atomicMin(A.fail + ch.sc, first_bad);
+    atomicAdd(A.viscall + ch.sc, (unsigned long long)vis);
   }
+}
+
+__global__ __launch_bounds__(64) void peak_write(SplitArgs A, const int32_t *pv) {
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall S = A.split[ch.sc];
+  const int32_t i = ch.start + (int32_t)threadIdx.x;
+  if (i < S.n) A.peak[S.off + i] = pv[64 * blockIdx.x + threadIdx.x];
+}
+
+// targets of a split call: segment 0's own marks (anchors < c1) merged with the split anchors'
+// marks by maximum (the last marker is the largest i); its visited pairs into the total
+__global__ __launch_bounds__(256) void merge_targets(SplitArgs A) {
+  const SplitCall S = A.split[blockIdx.x];
+  int32_t *tg = A.target + S.off;
+  const int32_t *t2 = A.t2 + S.off;
+  for (int32_t x = threadIdx.x; x < S.n; x += 256) tg[x] = x < S.c1 ? max(tg[x], t2[x]) : t2[x];
+  if (threadIdx.x == 0) atomicAdd(A.visited, A.viscall[blockIdx.x]);
 }
 
 namespace {
@@ -320,6 +336,8 @@ SplitArgs split_args(gb_chain_batch *B) {
   A.s_score = B->d_sscore;
   A.s_parent = B->d_sparent;
   A.visited = B->d_vis;
+  A.t2 = B->d_t2;
+  A.viscall = B->d_viscall;
   const char *f = getenv("GB_CHAIN_SPLIT_FAULT");
   A.fault = f ? atoi(f) : 0;
   return A;
@@ -366,6 +384,12 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   // host_kernel.cpp:57-58) and whether x is sorted; calls in parallel
   std::vector<int32_t> maxwin((size_t)ncalls, 0);
   std::vector<uint8_t> sorted((size_t)ncalls, 0);
+  // split candidates (>= 2 segments): st(i) kept, and per segment its warm-up start and widest
+  // window, all computed in the parallel pass
+  struct Cand {
+    std::vector<int32_t> st, as, win;
+  };
+  std::vector<Cand> cand((size_t)ncalls);
   auto walk = [&](int64_t c, int32_t *stw) {
     const int64_t off = offsets[c];
     const int32_t n = (int32_t)(offsets[c + 1] - off);
@@ -388,31 +412,48 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     std::vector<std::thread> th;
     for (int t = 0; t < nt; t++)
       th.emplace_back([&, t] {
-        for (int64_t c = t; c < ncalls; c += nt) walk(c, nullptr);
+        for (int64_t c = t; c < ncalls; c += nt) {
+          const int32_t n = (int32_t)(offsets[c + 1] - offsets[c]);
+          if (seg < 64 || (int64_t)n < 2 * (int64_t)seg) {
+            walk(c, nullptr);
+            continue;
+          }
+          Cand &K = cand[(size_t)c];
+          K.st.resize((size_t)n);
+          walk(c, K.st.data());
+          if (!sorted[(size_t)c]) {
+            K.st = std::vector<int32_t>();
+            continue;
+          }
+          const int32_t nseg = n / seg;
+          K.as.resize((size_t)nseg);
+          K.win.resize((size_t)nseg);
+          for (int32_t k = 0; k < nseg; k++) {
+            const int32_t cs = k * seg, es = k + 1 == nseg ? n : (k + 1) * seg;
+            const int32_t a = k == 0 ? 0 : std::max(0, K.st[(size_t)cs] - warm);
+            int32_t w = 0;
+            for (int32_t i = a; i < es; i++) w = std::max(w, i - std::max(a, K.st[(size_t)i]));
+            K.as[(size_t)k] = a;
+            K.win[(size_t)k] = w;
+          }
+        }
       });
     for (auto &t : th) t.join();
   }
   auto vpush = [&](int64_t in, int64_t out, int32_t n, int64_t c, int32_t mode, int32_t win) {
     B->vc.push_back({in, out, n, (int32_t)c, 0, mode, 0, win <= kRingSmall ? 1 : 0});
   };
-  std::vector<int32_t> stw;
   for (int64_t c = 0; c < ncalls; c++) {
     const int64_t off = offsets[c];
     const int32_t n = (int32_t)(offsets[c + 1] - off);
-    bool split = seg >= 64 && (int64_t)n >= 2 * (int64_t)seg && sorted[(size_t)c];
+    const Cand &K = cand[(size_t)c];
+    bool split = !K.as.empty();
     // the chunk space (64 * chunks) is indexed with int32
     if (split && 64 * ((int64_t)B->chunks.size() + n / 64 + 1) >= INT32_MAX) split = false;
     if (!split) {
       vpush(off, off, n, c, kVFinal, maxwin[(size_t)c]);
       continue;
     }
-    stw.resize((size_t)n);
-    walk(c, stw.data());
-    auto win = [&](int32_t a, int32_t e) {
-      int32_t w = 0;
-      for (int32_t i = a; i < e; i++) w = std::max(w, i - std::max(a, stw[(size_t)i]));
-      return w;
-    };
     SplitCall S;
     S.off = off;
     S.n = n;
@@ -421,23 +462,23 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     S.nseg = n / seg;
     S.c1 = seg;
     S.cbase = (int32_t)B->chunks.size();
-    vpush(off, off, seg, c, kVFinal, win(0, seg));  // segment 0: exact
+    vpush(off, off, seg, c, kVFinal, K.win[0]);  // segment 0: exact
     B->segs.push_back({0, seg, 0, 0, -1});
     for (int32_t k = 1; k < S.nseg; k++) {
       Seg G;
       G.cs = k * seg;
       G.es = k + 1 == S.nseg ? n : (k + 1) * seg;
-      G.as = std::max(0, stw[(size_t)G.cs] - warm);
+      G.as = K.as[(size_t)k];
       G.pad = 0;
       G.soff = B->scratch_n;
       B->scratch_n += G.es - G.as;
-      vpush(off + G.as, G.soff, G.es - G.as, c, kVScratch, win(G.as, G.es));
+      vpush(off + G.as, G.soff, G.es - G.as, c, kVScratch, K.win[(size_t)k]);
       B->segs.push_back(G);
     }
     const int32_t sc = (int32_t)B->split.size();
     for (int32_t st0 = S.c1; st0 < n; st0 += 64) B->chunks.push_back({sc, st0});
     B->st.resize(64 * B->chunks.size(), 0);
-    for (int32_t i = S.c1; i < n; i++) B->st[(size_t)64 * S.cbase + (size_t)(i - S.c1)] = stw[(size_t)i];
+    std::copy(K.st.begin() + S.c1, K.st.end(), B->st.begin() + (size_t)64 * S.cbase);
     B->split.push_back(S);
     B->max_split_n = std::max(B->max_split_n, n);
   }
@@ -464,6 +505,8 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   if (!st) st = grow(&B->d_sscore, &B->cap_sscore, B->scratch_n);
   if (!st) st = grow(&B->d_sparent, &B->cap_sparent, B->scratch_n);
   if (!st) st = grow(&B->d_front, &B->cap_front, 2 * ns);
+  if (!st) st = grow(&B->d_viscall, &B->cap_viscall, ns);
+  if (!st) st = grow(&B->d_t2, &B->cap_t2, B->nanchors);
   if (st) return st;
   B->d_fail = B->d_front + ns;
   {
@@ -496,9 +539,12 @@ int split_resolve(gb_chain_batch *B) {
   std::vector<int32_t> front((size_t)ns), fail((size_t)ns);
   for (int64_t k = 0; k < ns; k++) front[(size_t)k] = B->split[(size_t)k].c1;
   GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
+  GB_HIP(hipMemsetAsync(B->d_t2, 0, (size_t)B->nanchors * 4, B->stream));
+  GB_HIP(hipMemsetAsync(B->d_viscall, 0, (size_t)ns * 8, B->stream));
   const SplitArgs A = split_args(B);
   const int rounds = jump_rounds(B->max_split_n);
   std::vector<VCall> fix;
+  std::vector<uint8_t> failed((size_t)ns, 0);
   B->spec_rounds = 0;
   B->fixups = 0;
   while (true) {
@@ -507,7 +553,7 @@ int split_resolve(gb_chain_batch *B) {
     const int r = jump(B, 0, rounds);
     hipLaunchKernelGGL(guess_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
     GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
-    hipLaunchKernelGGL(verify_kernel<0>, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)nullptr);
+    hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A);
     GB_HIP(hipGetLastError());
     GB_HIP(hipMemcpyAsync(fail.data(), B->d_fail, (size_t)ns * 4, hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
@@ -519,6 +565,7 @@ int split_resolve(gb_chain_batch *B) {
         continue;
       }
       const SplitCall &S = B->split[(size_t)k];
+      failed[(size_t)k] = 1;
       const int32_t a0 = B->st[(size_t)64 * S.cbase + (size_t)(f - S.c1)];
       const int32_t e = std::min<int32_t>(S.n, f + kFix);
       fix.push_back({S.off + a0, S.off + a0, e - a0, S.call, f - a0, kVFixup, a0, 0});
@@ -533,9 +580,26 @@ int split_resolve(gb_chain_batch *B) {
     GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));  // the host vectors are reused next round
   }
+  // calls that ever failed: their marks and visited counts include wrong loops; redo them whole
+  bool redo = false;
+  for (int64_t k = 0; k < ns; k++) {
+    const SplitCall &S = B->split[(size_t)k];
+    front[(size_t)k] = failed[(size_t)k] ? S.c1 : S.n;
+    if (failed[(size_t)k]) {
+      redo = true;
+      GB_HIP(hipMemsetAsync(B->d_t2 + S.off, 0, (size_t)S.n * 4, B->stream));
+      GB_HIP(hipMemsetAsync(B->d_viscall + k, 0, 8, B->stream));
+    }
+  }
+  if (redo) {
+    GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
+    hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A);
+    GB_HIP(hipStreamSynchronize(B->stream));  // `front` is a host vector about to go
+  }
   hipLaunchKernelGGL(peak_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
   const int r = jump(B, 1, rounds);
-  hipLaunchKernelGGL(verify_kernel<1>, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+  hipLaunchKernelGGL(peak_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+  hipLaunchKernelGGL(merge_targets, dim3((unsigned)ns), dim3(256), 0, B->stream, A);
   GB_HIP(hipGetLastError());
   return GB_OK;
 }
@@ -543,7 +607,8 @@ int split_resolve(gb_chain_batch *B) {
 void split_free(gb_chain_batch *B) {
   for (void *p : {(void *)B->d_vc, (void *)B->d_split, (void *)B->d_segs, (void *)B->d_chunks, (void *)B->d_st,
                   (void *)B->d_sscore, (void *)B->d_sparent, (void *)B->d_front, (void *)B->d_link[0],
-                  (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1]})
+                  (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1], (void *)B->d_t2,
+                  (void *)B->d_viscall})
     (void)hipFree(p);
   B->d_vc = nullptr;
 }
