@@ -92,6 +92,28 @@ def test_phmm_gpu_edges_bit_exact():
 
 
 @pytest.mark.gpu
+def test_phmm_gpu_longest_haplotype():
+    """Haplotypes up to kMaxHaplen = 9400 columns (the f64 pass's LDS: 17 bytes per column) are
+    bit-exact; one column more is refused with GB_ERR_ARG (the GKL drop-in then aborts, as documented
+    in include/gb_phmm.h)."""
+    from genomicsbench_palisade_amd import GbError, phmm, set_device
+    set_device(0)
+    phmm.init_pairhmm()
+    rng = np.random.default_rng(11)
+    src = rng.choice(ALPHABET[:4], size=9401)
+    qs = tuple(bytes(v) for v in ([30] * 12, [45] * 12, [45] * 12, [10] * 12))
+    ok = TestcaseArray.from_pairs([((src[500:512].tobytes(),) + qs, src[:9400].tobytes()),
+                                   ((src[9000:9012].tobytes(),) + qs, src[:9400].tobytes())])
+    got = phmm.compute_likelihoods_both(ok)
+    exp = phmm_oracle(ok)
+    for k in range(3):
+        assert (bits(got[k]) == bits(exp[k])).all()
+    too_long = TestcaseArray.from_pairs([((src[:12].tobytes(),) + qs, src[:9401].tobytes())])
+    with pytest.raises(GbError):
+        phmm.compute_likelihoods_both(too_long)
+
+
+@pytest.mark.gpu
 def test_phmm_gpu_empty_batch():
     from genomicsbench_palisade_amd import phmm, set_device
     set_device(0)
