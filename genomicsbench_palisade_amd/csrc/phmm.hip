@@ -29,6 +29,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -672,8 +673,20 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   std::unordered_map<ReadKey, uint32_t, KeyHash> read_at;
   std::unordered_map<HapKey, uint32_t, KeyHash> hap_at;
   std::vector<TcDesc> desc(n);
+  std::vector<uint32_t> hid(n);  // dense haplotype index of each testcase (stack grouping)
+  std::vector<uint32_t> hap_off_of;
   int max_h = 0;
   int64_t cells = 0;
+  // the reference driver's r-major loop repeats a read for every haplotype and cycles the
+  // haplotypes: a last-read check and a small direct-mapped haplotype cache skip most hash lookups
+  ReadKey last_rk{nullptr, nullptr, nullptr, nullptr, nullptr, -1};
+  uint32_t last_roff = 0;
+  struct HapSlot {
+    const char *h = nullptr;
+    int len = -1;
+    uint32_t id = 0;
+  };
+  HapSlot hcache[256];
   for (int k = 0; k < n; k++) {
     const gb_testcase &t = tcs[k];
     GB_ARG(t.rslen >= 1 && t.rslen <= 65535, "testcase %d: rslen %d outside [1,65535]", k, t.rslen);
@@ -681,9 +694,11 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
            t.haplen, kMaxHaplen);
     GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
     const ReadKey rk{t.rs, t.q, t.i, t.d, t.c, t.rslen};
-    auto ri = read_at.find(rk);
     uint32_t roff;
-    if (ri != read_at.end()) {
+    auto ri = rk == last_rk ? read_at.end() : read_at.find(rk);
+    if (rk == last_rk) {
+      roff = last_roff;
+    } else if (ri != read_at.end()) {
       roff = ri->second;
     } else {
       roff = (uint32_t)pool.size();
@@ -698,17 +713,31 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       }
       read_at.emplace(rk, roff);
     }
+    last_rk = rk;
+    last_roff = roff;
     const HapKey hk{t.hap, t.haplen};
-    auto hi = hap_at.find(hk);
-    uint32_t hoff;
-    if (hi != hap_at.end()) {
-      hoff = hi->second;
+    HapSlot &hs = hcache[(((uintptr_t)t.hap) >> 4) & 255];
+    uint32_t id;
+    if (hs.h == t.hap && hs.len == t.haplen) {
+      id = hs.id;
     } else {
-      hoff = (uint32_t)pool.size();
-      pool.resize(pool.size() + (size_t)t.haplen);
-      for (int c = 0; c < t.haplen; c++) pool[hoff + c] = base_code(t.hap[c]);
-      hap_at.emplace(hk, hoff);
+      auto hi = hap_at.find(hk);
+      if (hi != hap_at.end()) {
+        id = hi->second;
+      } else {
+        id = (uint32_t)hap_off_of.size();
+        const uint32_t hoff = (uint32_t)pool.size();
+        pool.resize(pool.size() + (size_t)t.haplen);
+        for (int c = 0; c < t.haplen; c++) pool[hoff + c] = base_code(t.hap[c]);
+        hap_at.emplace(hk, id);
+        hap_off_of.push_back(hoff);
+      }
+      hs.h = t.hap;
+      hs.len = t.haplen;
+      hs.id = id;
     }
+    const uint32_t hoff = hap_off_of[id];
+    hid[k] = id;
     GB_ARG(pool.size() < (1ull << 32), "batch pool exceeds 4 GiB");
     desc[k].read_off = roff;
     desc[k].hap_off = hoff;
@@ -721,8 +750,12 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   // testcase) and 64 testcases; longest-processing-time first (the dispatcher hands out workgroups
   // in grid order).
   std::vector<int> order(n);
-  for (int k = 0; k < n; k++) order[k] = k;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return desc[a].hap_off < desc[b].hap_off; });
+  {  // counting sort by haplotype (stable: testcases keep their order within a haplotype)
+    std::vector<int> first(hap_off_of.size() + 1, 0);
+    for (int k = 0; k < n; k++) first[hid[k] + 1]++;
+    for (size_t h = 0; h < hap_off_of.size(); h++) first[h + 1] += first[h];
+    for (int k = 0; k < n; k++) order[first[hid[k]]++] = k;
+  }
   std::vector<Stack> stacks;
   std::vector<uint64_t> scost;
   for (int k = 0; k < n;) {
@@ -913,12 +946,23 @@ int gb_phmm_batch_results(gb_phmm_batch *b, double *results, float *raw_f, doubl
   if (dev_results) GB_HIP(hipMemcpy(dev_results, b->d_out, sizeof(double) * n, hipMemcpyDeviceToHost));
   const float l10f = b->tabs->hf.log10_init;
   const double l10d = b->tabs->hd.log10_init;
-  for (int k = 0; k < n; k++) {
-    const bool ud = rf[k] < 1e-28f;
-    if (results) results[k] = ud ? (log10(rd[k]) - l10d) : (double)(log10f(rf[k]) - l10f);
-    if (raw_f) raw_f[k] = rf[k];
-    if (raw_d) raw_d[k] = rd[k];
-    if (used_double) used_double[k] = ud ? 1 : 0;
+  auto part = [&](int lo, int hi) {
+    for (int k = lo; k < hi; k++) {
+      const bool ud = rf[k] < 1e-28f;
+      if (results) results[k] = ud ? (log10(rd[k]) - l10d) : (double)(log10f(rf[k]) - l10f);
+      if (raw_f) raw_f[k] = rf[k];
+      if (raw_d) raw_d[k] = rd[k];
+      if (used_double) used_double[k] = ud ? 1 : 0;
+    }
+  };
+  // the host log10 epilogue (bit-exact, unlike the device one) over a few threads for big jobs
+  const int nt = n >= (1 << 16) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  if (nt == 1) {
+    part(0, n);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) th.emplace_back(part, (int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt));
+    for (auto &t : th) t.join();
   }
   return GB_OK;
 }
