@@ -45,7 +45,7 @@ constexpr int kMaxHaplen = 9400;
 constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_stripe reads)
 constexpr int kRecPad = 4;   // boundary records below column 0 (lane 63's writes start at column -2)
 constexpr int kQualTab = 128;
-constexpr int kStackRows = 1024;  // rows per stack (a testcase taller than this gets its own)
+constexpr int kStackRows = 2048;  // rows per stack (a testcase taller than this gets its own)
 constexpr int kM2M = ((127 * 128) >> 1) + 128;  // set_mm_prob indices for quals < 128
 
 // ---------------------------------------------------------------------------------------------
