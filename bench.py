@@ -241,6 +241,35 @@ def _cores():
         return os.cpu_count() or 1
 
 
+def cpu_host():
+    """The host the CPU baselines ran on (nproc, affinity, model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": _cores(), "model": model,
+            "note": "cpu_baseline.cores = threads used (<= 16, the GPU box's CPU share per GPU); "
+                    "per_core = value / cores"}
+
+
+def add_per_core(obj):
+    """cpu_baseline objects (nested ones too) get value per thread used."""
+    if isinstance(obj, dict):
+        if "cpu_baseline" in obj and isinstance(obj["cpu_baseline"], dict):
+            cb = obj["cpu_baseline"]
+            if cb.get("value") and cb.get("cores"):
+                cb["per_core"] = cb["value"] / cb["cores"]
+            if isinstance(cb.get("port"), dict) and cb["port"].get("value") and cb["port"].get("cores"):
+                cb["port"]["per_core"] = cb["port"]["value"] / cb["port"]["cores"]
+        for v in obj.values():
+            add_per_core(v)
+
+
 def cpu_baseline_chain(calls, sample_seconds: float):
     """The reference's scalar chain_dp (tools/minimap2-acceleration/kernel/scalar, compiled from the
     reference tree into oracle/_ref, kind 'reference'; the C restatement when absent, kind 'port')
@@ -904,7 +933,9 @@ def main():
             "chain": ch,
             "bsw": bw,
             "small": small,
+            "cpu_host": cpu_host() if not args.no_cpu_baseline else None,
         }
+        add_per_core(line)
         print(json.dumps(line))
     D.close()
 

@@ -37,33 +37,9 @@ constexpr int kCap = 40;       // first-pass SMEM slots per read (~8 on average 
 constexpr int kBigCap = 2048;  // second pass, for the rare reads that overflow the first
 constexpr int kMaxOvf = 16384; // reads the second pass can take
 
-struct Ent {  // one `prev` entry (SMEM without rid), unpacked in registers
-  int64_t k, l, s;
-  uint32_t m, n;
-};
-
-// In memory an entry is 16 bytes: k, l, s < 2^34 rows and m, n < 2^13 read positions (checked on
-// the host), laid out wave-interleaved (entry e of lane t of wave w at [(w * stride + e) * 64 + t])
-// so the lanes of a wave touching the same list depth hit the same lines.
-struct __attribute__((aligned(16))) PEnt {
-  uint64_t w0, w1;
-};
-__device__ __forceinline__ PEnt pack_ent(const Ent &e) {
-  PEnt p;
-  p.w0 = (uint64_t)e.k | ((uint64_t)e.l << 34);
-  p.w1 = ((uint64_t)e.l >> 30) | ((uint64_t)e.s << 4) | ((uint64_t)e.m << 38) | ((uint64_t)e.n << 51);
-  return p;
-}
-__device__ __forceinline__ Ent unpack_ent(const PEnt &p) {
-  constexpr uint64_t M34 = (1ull << 34) - 1, M13 = (1ull << 13) - 1;
-  Ent e;
-  e.k = (int64_t)(p.w0 & M34);
-  e.l = (int64_t)((p.w0 >> 34) | ((p.w1 & 0xFull) << 30));
-  e.s = (int64_t)((p.w1 >> 4) & M34);
-  e.m = (uint32_t)((p.w1 >> 38) & M13);
-  e.n = (uint32_t)((p.w1 >> 51) & M13);
-  return e;
-}
+// `prev` entries (Ent / PEnt, fmi_index.h) are laid out wave-interleaved (entry e of lane t of
+// wave w at [(w * stride + e) * 64 + t]) so the lanes of a wave touching the same list depth hit the
+// same lines.
 struct PList {  // one lane's view of its wave-interleaved scratch
   PEnt *base;   // &scratch[(wave * stride) * 64 + lane]
   __device__ __forceinline__ Ent get(int e) const { return unpack_ent(base[(size_t)e * 64]); }
@@ -99,12 +75,10 @@ __global__ void compress_occ(const CpOcc *__restrict__ occ, int64_t cp_size, Occ
                                                                  : 3;
     w[r >> 5] |= code << (2 * (r & 31));
   }
-  const uint64_t cA = (uint64_t)b.cp_count[0], cC = (uint64_t)b.cp_count[1], cG = (uint64_t)b.cp_count[2];
   Occ32 L;
   L.bwt[0] = w[0];
   L.bwt[1] = w[1];
-  L.cnt[0] = cA | (cC << 34);
-  L.cnt[1] = (cC >> 30) | (cG << 4);
+  occ32_pack_counts(b.cp_count[0], b.cp_count[1], b.cp_count[2], L.cnt);
   out[i] = L;
 }
 
@@ -784,6 +758,28 @@ int reads_device_smems(gb_fmi_reads *R, const gb_smem **d_smems, int64_t *n) {
 }  // namespace gbfmi
 
 extern "C" {
+
+int gb_fmi_debug_pack(int64_t n, const int64_t *ent, int64_t *ent_out, const int64_t *cnt, int64_t *cnt_out) {
+  GB_ARG(n >= 0 && (n == 0 || (ent && ent_out && cnt && cnt_out)), "gb_fmi_debug_pack: bad arguments");
+  for (int64_t i = 0; i < n; i++) {
+    gbfmi::Ent e;
+    e.k = ent[5 * i];
+    e.l = ent[5 * i + 1];
+    e.s = ent[5 * i + 2];
+    e.m = (uint32_t)ent[5 * i + 3];
+    e.n = (uint32_t)ent[5 * i + 4];
+    const gbfmi::Ent r = gbfmi::unpack_ent(gbfmi::pack_ent(e));
+    ent_out[5 * i] = r.k;
+    ent_out[5 * i + 1] = r.l;
+    ent_out[5 * i + 2] = r.s;
+    ent_out[5 * i + 3] = r.m;
+    ent_out[5 * i + 4] = r.n;
+    uint64_t w[2];
+    gbfmi::occ32_pack_counts(cnt[3 * i], cnt[3 * i + 1], cnt[3 * i + 2], w);
+    gbfmi::occ32_unpack_counts(w, cnt_out[3 * i], cnt_out[3 * i + 1], cnt_out[3 * i + 2]);
+  }
+  return GB_OK;
+}
 
 int gb_fmi_debug_prof(uint64_t out[8], int reset) {
   GB_ARG(out, "gb_fmi_debug_prof: null out");

@@ -27,6 +27,44 @@ static_assert(sizeof(Occ32) == 32, "Occ32 is 32 bytes");
 
 constexpr uint64_t kEven = 0x5555555555555555ull;
 
+// The A, C, G counts of an Occ32 block: three 34-bit fields (rows < 2^34).
+__host__ __device__ __forceinline__ void occ32_pack_counts(int64_t cA, int64_t cC, int64_t cG, uint64_t cnt[2]) {
+  cnt[0] = (uint64_t)cA | ((uint64_t)cC << 34);
+  cnt[1] = ((uint64_t)cC >> 30) | ((uint64_t)cG << 4);
+}
+__host__ __device__ __forceinline__ void occ32_unpack_counts(const uint64_t cnt[2], int64_t &cA, int64_t &cC,
+                                                             int64_t &cG) {
+  cA = (int64_t)(cnt[0] & ((1ull << 34) - 1));
+  cC = (int64_t)((cnt[0] >> 34) | ((cnt[1] & 0xFull) << 30));
+  cG = (int64_t)((cnt[1] >> 4) & ((1ull << 34) - 1));
+}
+
+// One `prev` entry of the search (an SMEM without rid), unpacked in registers and 16 bytes in
+// memory: k, l, s < 2^34 rows and m, n < 2^13 read positions (checked on the host).
+struct Ent {
+  int64_t k, l, s;
+  uint32_t m, n;
+};
+struct __attribute__((aligned(16))) PEnt {
+  uint64_t w0, w1;
+};
+__host__ __device__ __forceinline__ PEnt pack_ent(const Ent &e) {
+  PEnt p;
+  p.w0 = (uint64_t)e.k | ((uint64_t)e.l << 34);
+  p.w1 = ((uint64_t)e.l >> 30) | ((uint64_t)e.s << 4) | ((uint64_t)e.m << 38) | ((uint64_t)e.n << 51);
+  return p;
+}
+__host__ __device__ __forceinline__ Ent unpack_ent(const PEnt &p) {
+  constexpr uint64_t M34 = (1ull << 34) - 1, M13 = (1ull << 13) - 1;
+  Ent e;
+  e.k = (int64_t)(p.w0 & M34);
+  e.l = (int64_t)((p.w0 >> 34) | ((p.w1 & 0xFull) << 30));
+  e.s = (int64_t)((p.w1 >> 4) & M34);
+  e.m = (uint32_t)((p.w1 >> 38) & M13);
+  e.n = (uint32_t)((p.w1 >> 51) & M13);
+  return e;
+}
+
 // A, C, G occurrences in rows [64b, p) of block b = p >> 6 plus the counts before the block.
 __device__ __forceinline__ void occ32_acg(const Occ32 &L, int64_t p, int64_t &oA, int64_t &oC, int64_t &oG) {
   const int y = (int)(p & 63);
@@ -35,9 +73,8 @@ __device__ __forceinline__ void occ32_acg(const Occ32 &L, int64_t p, int64_t &oA
   const uint64_t m1 = (((1ull << (2 * y1)) - 1) & kEven);  // y1 <= 31
   const uint64_t lo0 = L.bwt[0] & kEven, hi0 = (L.bwt[0] >> 1) & kEven;
   const uint64_t lo1 = L.bwt[1] & kEven, hi1 = (L.bwt[1] >> 1) & kEven;
-  const int64_t cA = (int64_t)(L.cnt[0] & ((1ull << 34) - 1));
-  const int64_t cC = (int64_t)((L.cnt[0] >> 34) | ((L.cnt[1] & 0xFull) << 30));
-  const int64_t cG = (int64_t)((L.cnt[1] >> 4) & ((1ull << 34) - 1));
+  int64_t cA, cC, cG;
+  occ32_unpack_counts(L.cnt, cA, cC, cG);
   oA = cA + __popcll(m0 & ~(lo0 | hi0)) + __popcll(m1 & ~(lo1 | hi1));
   oC = cC + __popcll(m0 & lo0 & ~hi0) + __popcll(m1 & lo1 & ~hi1);
   oG = cG + __popcll(m0 & hi0 & ~lo0) + __popcll(m1 & hi1 & ~lo1);

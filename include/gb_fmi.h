@@ -135,6 +135,12 @@ int gb_fmi_sa_one_step(gb_fmi_index *idx, int64_t pos, int64_t *sa_entry, int64_
  * which a lane took a new read, state-machine clocks of those trips, 0}; reset != 0 zeroes them. */
 int gb_fmi_debug_prof(uint64_t out[8], int reset);
 
+/* Diagnostic, host only (no device work): round trips through the search's packed layouts, the
+ * code the kernels run. ent: n entries of {k, l, s, m, n} (k, l, s < 2^34; m, n < 2^13) packed into
+ * 16-byte `prev` entries and back into ent_out; cnt: n triples {A, C, G} (< 2^34) packed into an
+ * Occ32 block's count words and back into cnt_out. */
+int gb_fmi_debug_pack(int64_t n, const int64_t *ent, int64_t *ent_out, const int64_t *cnt, int64_t *cnt_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,3 +169,29 @@ def test_bwa_v1_over_cp_occ_tables_matches_oracle(tmp_path):
     assert fmi_util.bwa_collect_threaded(lib, bwt, codes, lens, 3) == len(exp)
     lib.ref_bwa_free(bwt)
     oi.close()
+
+
+def test_packed_layouts_above_2_32():
+    """The search's 16-byte `prev` entries and Occ32 count words (csrc/fmi_index.h) hold row values up
+    to 2^34 - 1, i.e. indexes of > 2^32 BWT rows (a human genome's 6.2 G rows): host round trip
+    through the same inline functions the kernels use (gb_fmi_debug_pack, no device work)."""
+    import ctypes
+    from genomicsbench_palisade_amd import lib
+    L = lib()
+    L.gb_fmi_debug_pack.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4
+    rng = np.random.default_rng(5)
+    top = (1 << 34) - 1
+    rows = np.array([0, 1, (1 << 31) - 1, 1 << 31, (1 << 32) - 1, 1 << 32, (1 << 32) + 12345, 6_200_000_001, top - 1, top],
+                    np.int64)
+    n = 400
+    ent = np.zeros((n, 5), np.int64)
+    ent[:, :3] = rng.choice(rows, size=(n, 3))
+    ent[: len(rows), 0] = rows
+    ent[: len(rows), 1] = rows[::-1]
+    ent[: len(rows), 2] = rows
+    ent[:, 3] = rng.integers(0, 1 << 13, n)
+    ent[:, 4] = rng.integers(0, 1 << 13, n)
+    cnt = rng.choice(rows, size=(n, 3)).astype(np.int64)
+    eo, co = np.zeros_like(ent), np.zeros_like(cnt)
+    assert L.gb_fmi_debug_pack(n, ent.ctypes.data, eo.ctypes.data, cnt.ctypes.data, co.ctypes.data) == 0
+    assert (eo == ent).all() and (co == cnt).all()
