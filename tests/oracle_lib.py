@@ -5,7 +5,8 @@ import ctypes
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+# GB_ORACLE_SO selects another build of the same sources (tools/sanitize.sh: ASan + UBSan)
+ORACLE_SO = os.environ.get("GB_ORACLE_SO") or os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 REF_PHMM_SO = os.path.join(ROOT, "oracle", "_ref", "libref_phmm.so")
 
 _oracle = None
