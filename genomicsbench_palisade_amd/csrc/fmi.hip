@@ -668,6 +668,11 @@ struct gb_fmi_reads {
   bool scattered = false;  // d_out holds the last search's compacted SMEMs
   int64_t total = 0;
   gbfmi::SaJob *sa = nullptr;
+  // grow-only capacities (bytes): a destroyed read set goes back to its thread's free list with its
+  // stream and buffers, and the next create reuses them (no hipMalloc / hipFree per batch)
+  int device = -1;
+  size_t cap_qdb = 0, cap_q4 = 0, cap_lens = 0, cap_scratch = 0, cap_slots = 0, cap_ovf_pos = 0, cap_counts = 0,
+         cap_phase = 0, cap_offsets = 0, cap_temp = 0;
 };
 
 namespace {
@@ -896,6 +901,17 @@ int gb_fmi_index_destroy(gb_fmi_index *idx) {
   return GB_OK;
 }
 
+}  // extern "C"
+
+// Destroyed read sets of this thread, kept for reuse (never freed: freeing at thread exit could
+// run after the HIP runtime is torn down).
+static std::vector<gb_fmi_reads *> &free_reads() {
+  thread_local std::vector<gb_fmi_reads *> fl;
+  return fl;
+}
+
+extern "C" {
+
 int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens,
                         int32_t num_reads, int32_t max_readlength, gb_fmi_reads **out) {
   GB_ARG(idx && out && (num_reads == 0 || (enc_qdb && lens)), "gb_fmi_reads_create: null argument");
@@ -906,33 +922,59 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     GB_ARG(lens[r] >= 0 && lens[r] <= max_readlength, "read %d: length %d > max_readlength %d", r,
            lens[r], max_readlength);
   *out = nullptr;
-  auto *R = new gb_fmi_reads();
+  int dev = 0;
+  GB_HIP(hipGetDevice(&dev));
+  gb_fmi_reads *R = nullptr;
+  {
+    auto &fl = free_reads();
+    for (size_t k = 0; k < fl.size(); k++)
+      if (fl[k]->device == dev) {
+        R = fl[k];
+        fl.erase(fl.begin() + (long)k);
+        break;
+      }
+  }
+  hipError_t e = hipSuccess;
+  if (!R) {
+    R = new gb_fmi_reads();
+    R->device = dev;
+    e = hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking);
+    for (auto &ev : R->ev)
+      if (e == hipSuccess) e = hipEventCreate(&ev);
+    if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&R->d_big, (size_t)gbfmi::kMaxOvf * gbfmi::kBigCap * sizeof(gb_smem));
+    if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 4 * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&R->d_calls, 2 * sizeof(unsigned long long));
+  }
   R->idx = idx;
   R->nreads = num_reads;
   R->stride = max_readlength;
   R->lanes = lanes_for_device();
+  R->ran = R->scattered = false;
+  R->total = 0;
   const size_t nr = (size_t)std::max(num_reads, 1);
-  hipError_t e = hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking);
-  for (auto &ev : R->ev)
-    if (e == hipSuccess) e = hipEventCreate(&ev);
-  if (e == hipSuccess) e = hipMalloc(&R->d_qdb, nr * (size_t)max_readlength);
-  if (e == hipSuccess) e = hipMalloc(&R->d_lens, nr * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::PEnt));
-  if (e == hipSuccess) e = hipMalloc(&R->d_slots, nr * gbfmi::kCap * sizeof(gb_smem));
-  if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_ovf_pos, nr * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_big, (size_t)gbfmi::kMaxOvf * gbfmi::kBigCap * sizeof(gb_smem));
-  if (e == hipSuccess) e = hipMalloc(&R->d_counts, nr * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_phase, nr * 3 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_offsets, (nr + 1) * sizeof(int64_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 4 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&R->d_calls, 2 * sizeof(unsigned long long));
+  auto reserve = [&](auto **p, size_t *cap, size_t bytes) {
+    if (e != hipSuccess || bytes <= *cap) return;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    e = hipMalloc(p, std::max<size_t>(bytes, 16));
+    if (e == hipSuccess) *cap = bytes;
+  };
+  reserve(&R->d_qdb, &R->cap_qdb, nr * (size_t)max_readlength);
+  reserve(&R->d_lens, &R->cap_lens, nr * sizeof(int32_t));
+  reserve(&R->d_scratch, &R->cap_scratch, (size_t)R->lanes * max_readlength * sizeof(gbfmi::PEnt));
+  reserve(&R->d_slots, &R->cap_slots, nr * gbfmi::kCap * sizeof(gb_smem));
+  reserve(&R->d_ovf_pos, &R->cap_ovf_pos, nr * sizeof(int32_t));
+  reserve(&R->d_counts, &R->cap_counts, nr * sizeof(int32_t));
+  reserve(&R->d_phase, &R->cap_phase, nr * 3 * sizeof(int32_t));
+  reserve(&R->d_offsets, &R->cap_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess)
     e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
-  if (e == hipSuccess) e = hipMalloc(&R->d_temp, std::max<size_t>(R->temp_bytes, 16));
+  reserve(&R->d_temp, &R->cap_temp, std::max<size_t>(R->temp_bytes, 16));
   if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
   R->q4_stride = (((max_readlength + 7) / 8) + 3) & ~3;  // 16-byte rows (smem_search staging)
-  if (e == hipSuccess) e = hipMalloc(&R->d_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
+  reserve(&R->d_q4, &R->cap_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
   if (e == hipSuccess && num_reads) {
     const int64_t nt = (int64_t)num_reads * R->q4_stride;
     hipLaunchKernelGGL(gbfmi::pack_q4, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
@@ -954,6 +996,11 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   if (!R) return GB_OK;
   if (R->stream) (void)hipStreamSynchronize(R->stream);
   gbfmi::sa_job_destroy(R->sa);
+  R->sa = nullptr;
+  if (R->stream && R->d_big) {  // a complete read set: keep it for the next create on this thread
+    free_reads().push_back(R);
+    return GB_OK;
+  }
   for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
