@@ -881,7 +881,11 @@ def main():
     world, rank, local = dist_env()
     D = Dist(world)
     import genomicsbench_palisade_amd as gb
-    gb.set_device(local)
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a smaller box)
+    # share them round-robin. torch.cuda.device_count() does not initialise the GPU.
+    import torch
+    ndev = max(1, torch.cuda.device_count())
+    gb.set_device(local % ndev)
 
     legs = set((args.only or "phmm,fmi,chain,bsw").split(","))
     ph = bench_phmm(args, D, rank, world) if "phmm" in legs else None
