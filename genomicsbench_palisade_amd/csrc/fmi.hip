@@ -844,9 +844,9 @@ int gb_fmi_index_load(const char *path, gb_fmi_index **out) {
   idx->sa_ns = ns;
   hipError_t e = hipMalloc(&idx->d_occ, sizeof(gbfmi::CpOcc) * (size_t)cp_size);
   if (e == hipSuccess)
-    e = hipMemcpy(idx->d_occ, occ.data(), sizeof(gbfmi::CpOcc) * (size_t)cp_size, hipMemcpyHostToDevice);
+    e = gb::memcpy_big(idx->d_occ, occ.data(), sizeof(gbfmi::CpOcc) * (size_t)cp_size, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&idx->d_sa, sizeof(int64_t) * (size_t)ns);
-  if (e == hipSuccess) e = hipMemcpy(idx->d_sa, sa.data(), sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = gb::memcpy_big(idx->d_sa, sa.data(), sizeof(int64_t) * (size_t)ns, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     gb::set_error("gb_fmi_index_load: %s", hipGetErrorString(e));
     gb_fmi_index_destroy(idx);
@@ -880,7 +880,7 @@ int gb_fmi_index_cp_occ(gb_fmi_index *idx, void *dst, int64_t dst_bytes) {
   GB_ARG(idx && dst, "gb_fmi_index_cp_occ: null argument");
   const int64_t bytes = idx->cp_size * (int64_t)sizeof(gbfmi::CpOcc);
   GB_ARG(dst_bytes >= bytes, "gb_fmi_index_cp_occ: need %lld bytes", (long long)bytes);
-  GB_HIP(hipMemcpy(dst, idx->d_occ, (size_t)bytes, hipMemcpyDeviceToHost));
+  GB_HIP(gb::memcpy_big(dst, idx->d_occ, (size_t)bytes, hipMemcpyDeviceToHost));
   return GB_OK;
 }
 
@@ -888,7 +888,7 @@ int gb_fmi_index_sa(gb_fmi_index *idx, int64_t *dst, int64_t dst_entries) {
   GB_ARG(idx && dst, "gb_fmi_index_sa: null argument");
   GB_ARG(idx->d_sa, "gb_fmi_index_sa: index has no sampled suffix array");
   GB_ARG(dst_entries >= idx->sa_ns, "gb_fmi_index_sa: need %lld entries", (long long)idx->sa_ns);
-  GB_HIP(hipMemcpy(dst, idx->d_sa, sizeof(int64_t) * (size_t)idx->sa_ns, hipMemcpyDeviceToHost));
+  GB_HIP(gb::memcpy_big(dst, idx->d_sa, sizeof(int64_t) * (size_t)idx->sa_ns, hipMemcpyDeviceToHost));
   return GB_OK;
 }
 
@@ -972,7 +972,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   if (e == hipSuccess)
     e = hipcub::DeviceScan::ExclusiveSum(nullptr, R->temp_bytes, R->d_counts, R->d_offsets, (int)nr);
   reserve(&R->d_temp, &R->cap_temp, std::max<size_t>(R->temp_bytes, 16));
-  if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
+  if (e == hipSuccess && num_reads) e = gb::memcpy_big(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
   R->q4_stride = (((max_readlength + 7) / 8) + 3) & ~3;  // 16-byte rows (smem_search staging)
   reserve(&R->d_q4, &R->cap_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
   if (e == hipSuccess && num_reads) {
@@ -1118,8 +1118,8 @@ int gb_fmi_results(gb_fmi_reads *R, int32_t batch_size, gb_smem *out, int64_t ou
     GB_ARG(out_cap >= tot, "gb_fmi_results: out_cap %lld < %lld SMEMs", (long long)out_cap, (long long)tot);
     if (int st = gbfmi::scatter_out(R, tot)) return st;
     if (tot) {
-      GB_HIP(hipMemcpyAsync(out, R->d_out, sizeof(gb_smem) * (size_t)tot, hipMemcpyDeviceToHost, R->stream));
       GB_HIP(hipStreamSynchronize(R->stream));
+      GB_HIP(gb::memcpy_big(out, R->d_out, sizeof(gb_smem) * (size_t)tot, hipMemcpyDeviceToHost));
     }
   }
   return GB_OK;

@@ -300,7 +300,7 @@ int download(SaJob *J, int64_t *coords, int64_t coords_cap, int32_t *counts, int
     GB_ARG(coords_cap >= J->ncoords, "SA lookup: coords_cap %lld < %lld coordinates", (long long)coords_cap,
            (long long)J->ncoords);
     if (J->ncoords)
-      GB_HIP(hipMemcpy(coords, J->d_coords, sizeof(int64_t) * (size_t)J->ncoords, hipMemcpyDeviceToHost));
+      GB_HIP(gb::memcpy_big(coords, J->d_coords, sizeof(int64_t) * (size_t)J->ncoords, hipMemcpyDeviceToHost));
   }
   if (counts && J->nsmem) {
     std::vector<int64_t> c((size_t)J->nsmem);
@@ -357,7 +357,7 @@ int gb_fmi_sa_entries(gb_fmi_index *idx, const gb_smem *smems, int64_t n, int32_
   int st = job_create(nullptr, &J);
   if (!st) st = check_index(idx, J->stream);
   if (!st) st = grow(J->d_smems_own, J->smem_own_cap, n);
-  if (!st && n && hipMemcpy(J->d_smems_own, smems, sizeof(gb_smem) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+  if (!st && n && gb::memcpy_big(J->d_smems_own, smems, sizeof(gb_smem) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
     gb::set_error("gb_fmi_sa_entries: upload failed");
     st = GB_ERR_HIP;
   }

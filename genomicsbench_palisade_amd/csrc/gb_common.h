@@ -30,6 +30,18 @@ const char *last_error();
     }                              \
   } while (0)
 
+// Synchronous copy in pieces of at most 1 GiB, for the copies that can pass 4 GiB (index tables,
+// SMEM and coordinate read-backs): no single transfer's size field reaches 32 bits.
+inline hipError_t memcpy_big(void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  constexpr size_t kPiece = size_t(1) << 30;
+  for (size_t o = 0; o < bytes; o += kPiece) {
+    const size_t b = bytes - o < kPiece ? bytes - o : kPiece;
+    const hipError_t e = hipMemcpy(static_cast<char *>(dst) + o, static_cast<const char *>(src) + o, b, kind);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 // roctx range around a host entry point (visible in rocprofv3 --marker-trace; a no-op otherwise)
 struct Range {
   explicit Range(const char *name) { roctxRangePushA(name); }

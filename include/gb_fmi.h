@@ -39,7 +39,10 @@ typedef struct gb_fmi_index gb_fmi_index;
 int gb_fmi_index_load(const char *bwt_2bit_64_path, gb_fmi_index **out);
 /* build_index() on the GPU from forward-strand codes (0..3 = A,C,G,T; pac2nt order): text =
  * ref + reverse complement, suffix array, BWT, CP_OCC checkpoints, sampled SA. out_path (nullable)
- * receives the reference-format .bwt.2bit.64 file. */
+ * receives the reference-format .bwt.2bit.64 file. Text up to 2^34 - 2 rows (32-bit rows below 2^31,
+ * 64-bit above); env GB_FMI_BUILD_WIDE=1 forces the 64-bit path, GB_FMI_BUILD_CHUNK=<rows> (64 ..
+ * 2^30) caps the rows of one sort (tests). GB_ERR_ARG when more than that many suffixes share an
+ * 8-base prefix or a tied group. */
 int gb_fmi_index_build(const uint8_t *ref_codes, int64_t ref_len, const char *out_path,
                        gb_fmi_index **out);
 /* Builds the search-side Occ32 table now (otherwise the first search does); call it before host

@@ -241,3 +241,39 @@ def test_sa_edge_cases(fmi):
     rs2 = fmi.Reads(idx, codes, np.full(3, 50, np.int32))
     with pytest.raises(GbError):
         rs2.sa_run()  # not searched yet
+
+
+def _repeat_heavy_reference():
+    """Genome-like text plus long exact repeats (a 3 kb segment in four places, a 1.5 kb poly-A run,
+    an 800-base dinucleotide run): tied groups that need many doubling rounds and span chunks."""
+    ref = gen.fmi_reference(150_000, seed=21, repeat_frac=0.1)
+    seg = ref[5_000:8_000].copy()
+    for d in (20_000, 47_000, 90_000, 131_000):
+        ref[d:d + len(seg)] = seg
+    ref[60_000:61_500] = 0
+    ref[110_000:110_800] = np.resize(np.array([1, 2], np.uint8), 800)
+    return ref
+
+
+@pytest.mark.parametrize("wide,chunk", [("1", ""), ("0", "5000"), ("1", "3000"), ("0", "")])
+def test_gpu_index_build_chunked_and_wide(fmi, tmp_path, monkeypatch, wide, chunk):
+    """The bucketed first sort, whole-group doubling chunks and 64-bit rows (the builder's path above
+    2^31 rows), forced on a small repeat-heavy text, reproduce the reference index byte for byte."""
+    monkeypatch.setenv("GB_FMI_BUILD_WIDE", wide)
+    monkeypatch.setenv("GB_FMI_BUILD_CHUNK", chunk)
+    ref = _repeat_heavy_reference()
+    p_or, p_gpu = str(tmp_path / "o.bwt.2bit.64"), str(tmp_path / "g.bwt.2bit.64")
+    oi = fmi_util.OracleIndex(ref, path_out=p_or)
+    gi = fmi.Index.build(ref, out_path=p_gpu)
+    assert gi.info() == oi.info()
+    assert open(p_or, "rb").read() == open(p_gpu, "rb").read()
+    oi.close()
+    gi.close()
+
+
+def test_gpu_index_build_refuses_oversized_chunk_groups(fmi, monkeypatch):
+    # 64-suffix chunks cannot hold the ~1500 suffixes that start with eight A's (the poly-A run)
+    monkeypatch.setenv("GB_FMI_BUILD_CHUNK", "64")
+    from genomicsbench_palisade_amd import GbError
+    with pytest.raises(GbError, match="share one 8-base prefix"):
+        fmi.Index.build(_repeat_heavy_reference())

@@ -93,3 +93,60 @@ def test_large_index_and_search_vs_oracle():
     oi.close()
     rs.close()
     idx.close()
+
+
+HUGE_BP = 2_200_000_000  # text 4.4 G rows: SA values and rows above 2^32 (64-bit builder path)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_index_above_2_32_rows_and_search_vs_oracle():
+    """The builder past the 2^31 (32-bit) and 2^32 (sampled-SA ms byte) row limits, at a 2.2 Gbp
+    reference (a human-scale text is 6.4 G rows): the same invariants as the 'large' test, LF walks
+    from rows above 2^32, and the SMEM search over the built tables equal to the oracle's."""
+    from genomicsbench_palisade_amd import fmi, set_device
+    import time
+    set_device(0)
+    t0 = time.time()
+
+    def progress(what):  # long test: a line per phase
+        print(f"[{time.time() - t0:6.1f}s] {what}", flush=True)
+    ref = gen.fmi_reference(HUGE_BP, seed=31, repeat_frac=0.001)
+    ref[HUGE_BP // 2:HUGE_BP // 2 + 20_000] = 0  # a 20 kb poly-A run: ~10 doubling rounds
+    progress("reference generated")
+    idx = fmi.Index.build(ref)
+    progress("index built")
+    n, c5, sent = idx.info()
+    assert n == 2 * HUGE_BP + 1 and n > (1 << 32)
+    cp = idx.cp_occ()
+    sa = idx.sampled_sa()
+    assert sa.max() > (1 << 32)
+    fmi_util.check_index_structure(ref, n, c5, sent, cp, sa, sample=20000, seed=3)
+    progress("structure checked")
+    del sa
+    rng = np.random.default_rng(4)
+    rows = np.unique(np.concatenate([rng.integers(0, n - 1, 2000), rng.integers(1 << 32, n - 1, 2000),
+                                     np.arange(HUGE_BP - 5, HUGE_BP + 5)]))
+    got = idx.sa_lookup(np.concatenate([rows, rows + 1]))
+    s0, s1 = got[:len(rows)], got[len(rows):]
+    text = np.concatenate([ref, (3 - ref[::-1]).astype(np.uint8)])
+    assert fmi_util.suffix_less(text, s0, s1).all()
+    assert (fmi_util.bwt_char(cp, rows) == np.where(s0 > 0, text[np.maximum(s0 - 1, 0)], 4)).all()
+    del text
+    progress("LF walks checked")
+    codes, lens = gen.fmi_reads(ref, 4_000, read_len=151, seed=9)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(19)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    _, _, calls = rs.timing()
+    oi = fmi_util.OracleIndex(adopt=(n, c5, sent, cp))
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512)
+    progress("search compared")
+    assert tot == len(exp) and tot > 0
+    assert (bc == ebc).all() and (pc == epc).all()
+    for f in ("rid", "m", "n", "k", "l", "s"):
+        assert (sm[f] == exp[f]).all(), f
+    assert calls == oi.bwt_calls()
+    oi.close()
+    rs.close()
+    idx.close()
