@@ -534,6 +534,10 @@ struct gb_bsw_batch {
   unsigned long long *d_prof = nullptr;  // GB_BSW_PROF=1 per-variant sweep counters (development aid)
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  // the variants' launches run side by side: each on its own stream, forked from and joined back
+  // into `stream` (a small batch fills the chip only when its short launches overlap)
+  hipStream_t side[kVariants] = {};
+  hipEvent_t fork = nullptr, join[kVariants] = {};
   gb_bsw_params params{};
   int64_t n = 0;
   gbbsw::Pair *d_pairs = nullptr;
@@ -575,6 +579,11 @@ int gb_bsw_batch_destroy(gb_bsw_batch *B) {
     (void)hipFree(p);
   for (auto &e : B->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto &e : B->join)
+    if (e) (void)hipEventDestroy(e);
+  if (B->fork) (void)hipEventDestroy(B->fork);
+  for (auto &s : B->side)
+    if (s) (void)hipStreamDestroy(s);
   if (B->stream) (void)hipStreamDestroy(B->stream);
   delete B;
   return GB_OK;
@@ -591,6 +600,11 @@ int bsw_batch_new(gb_bsw_batch **out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking);
   for (auto &ev : B->ev)
     if (e == hipSuccess) e = hipEventCreate(&ev);
+  for (auto &s : B->side)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  for (auto &ev : B->join)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&B->fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&B->d_total, 2 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     gb::set_error("gb_bsw_batch_create: %s", hipGetErrorString(e));
@@ -719,6 +733,7 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
   GB_HIP(hipSetDevice(B->device));
   GB_HIP(hipMemsetAsync(B->d_total, 0, 2 * sizeof(unsigned long long), B->stream));
   GB_HIP(hipEventRecord(B->ev[0], B->stream));
+  bool forked[gb_bsw_batch::kVariants] = {};
   if (B->n > 0) {
     gbbsw::LaneArgs L;
     L.pairs = B->d_pairs;
@@ -752,12 +767,19 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
       if (!B->d_prof) GB_HIP(hipMalloc(&B->d_prof, 25 * sizeof(unsigned long long)));
       GB_HIP(hipMemsetAsync(B->d_prof, 0, 25 * sizeof(unsigned long long), B->stream));
     }
+    // variant v launches on side stream v, forked from `stream` here and joined back below
+    GB_HIP(hipEventRecord(B->fork, B->stream));
+    for (int v = 0; v < gb_bsw_batch::kVariants; ++v)
+      if (B->seg[v + 1] > B->seg[v]) {
+        GB_HIP(hipStreamWaitEvent(B->side[v], B->fork, 0));
+        forked[v] = true;
+      }
     for (int v = 0; v < 5; ++v) {
       if (prof) L.prof = B->d_prof + 5 * v;
       L.first = B->seg[v];
       L.count = B->seg[v + 1] - B->seg[v];
       if (L.count == 0) continue;
-      hipLaunchKernelGGL(lane_kernels[sym ? 1 : 0][v], dim3((unsigned)((L.count + 63) / 64)), dim3(64), 0, B->stream,
+      hipLaunchKernelGGL(lane_kernels[sym ? 1 : 0][v], dim3((unsigned)((L.count + 63) / 64)), dim3(64), 0, B->side[v],
                          L);
       GB_HIP(hipGetLastError());
     }
@@ -783,10 +805,15 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
       const int64_t cap = (int64_t)B->num_cus * gbbsw::kBlocksPerCU;
       const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cap, (nw + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
       hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0,
-                         B->stream, A);
+                         B->side[5], A);
       GB_HIP(hipGetLastError());
     }
   }
+  for (int v = 0; v < gb_bsw_batch::kVariants; ++v)
+    if (forked[v]) {
+      GB_HIP(hipEventRecord(B->join[v], B->side[v]));
+      GB_HIP(hipStreamWaitEvent(B->stream, B->join[v], 0));
+    }
   GB_HIP(hipEventRecord(B->ev[1], B->stream));
   B->ran = true;
   if (B->d_prof && getenv("GB_BSW_PROF")) {
