@@ -683,7 +683,9 @@ int lanes_for_device() {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
-  const int waves = e ? std::max(1, atoi(e)) : 16;
+  // 12 resident waves per CU (3 per SIMD): large set 29.99 vs 29.74 Mreads/s at 16, 'small' (1 M
+  // reads, ~5 per lane) 18.47 vs 17.62 -- fewer lanes, shorter per-wave tails (tools/fmi_small_occ.sh)
+  const int waves = e ? std::max(1, atoi(e)) : 12;
   return cus * waves * 64;
 }
 
