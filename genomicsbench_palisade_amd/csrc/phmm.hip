@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <unordered_map>
 #include <thread>
@@ -668,83 +669,152 @@ namespace {
 // device buffers when they are too small. b's stream/events exist already.
 int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
-  // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once.
-  std::vector<uint8_t> pool;
-  std::unordered_map<ReadKey, uint32_t, KeyHash> read_at;
-  std::unordered_map<HapKey, uint32_t, KeyHash> hap_at;
-  std::vector<TcDesc> desc(n);
-  std::vector<uint32_t> hid(n);  // dense haplotype index of each testcase (stack grouping)
-  std::vector<uint32_t> hap_off_of;
-  int max_h = 0;
-  int64_t cells = 0;
-  // the reference driver's r-major loop repeats a read for every haplotype and cycles the
-  // haplotypes: a last-read check and a small direct-mapped haplotype cache skip most hash lookups
-  ReadKey last_rk{nullptr, nullptr, nullptr, nullptr, nullptr, -1};
-  uint32_t last_roff = 0;
-  struct HapSlot {
-    const char *h = nullptr;
-    int len = -1;
-    uint32_t id = 0;
-  };
-  HapSlot hcache[256];
+  // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once. Inputs are validated
+  // first (sequentially, so the error names the first bad testcase), then big jobs pack in
+  // contiguous chunks on several threads, each with its own pool and maps; chunk pools are
+  // concatenated and haplotype ids are made global in first-appearance order, which is the id order
+  // a single pass gives (a read shared across a chunk edge is stored once per chunk).
   for (int k = 0; k < n; k++) {
     const gb_testcase &t = tcs[k];
     GB_ARG(t.rslen >= 1 && t.rslen <= 65535, "testcase %d: rslen %d outside [1,65535]", k, t.rslen);
     GB_ARG(t.haplen >= 1 && t.haplen <= kMaxHaplen, "testcase %d: haplen %d outside [1,%d]", k,
            t.haplen, kMaxHaplen);
     GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
-    const ReadKey rk{t.rs, t.q, t.i, t.d, t.c, t.rslen};
-    uint32_t roff;
-    auto ri = rk == last_rk ? read_at.end() : read_at.find(rk);
-    if (rk == last_rk) {
-      roff = last_roff;
-    } else if (ri != read_at.end()) {
-      roff = ri->second;
-    } else {
-      roff = (uint32_t)pool.size();
-      pool.resize(pool.size() + 5 * (size_t)t.rslen);
-      uint8_t *rec = pool.data() + roff;
-      for (int r = 0; r < t.rslen; r++) {
-        rec[r] = read_match_mask(base_code(t.rs[r]));
-        rec[t.rslen + r] = (uint8_t)t.q[r];
-        rec[2 * t.rslen + r] = (uint8_t)t.i[r];
-        rec[3 * t.rslen + r] = (uint8_t)t.d[r];
-        rec[4 * t.rslen + r] = (uint8_t)t.c[r];
-      }
-      read_at.emplace(rk, roff);
-    }
-    last_rk = rk;
-    last_roff = roff;
-    const HapKey hk{t.hap, t.haplen};
-    HapSlot &hs = hcache[(((uintptr_t)t.hap) >> 4) & 255];
-    uint32_t id;
-    if (hs.h == t.hap && hs.len == t.haplen) {
-      id = hs.id;
-    } else {
-      auto hi = hap_at.find(hk);
-      if (hi != hap_at.end()) {
-        id = hi->second;
+  }
+  std::vector<TcDesc> desc(n);
+  std::vector<uint32_t> hid(n);  // dense haplotype index of each testcase (stack grouping)
+  struct Chunk {
+    int lo = 0, hi = 0;
+    std::vector<uint8_t> pool;
+    std::vector<uint32_t> hap_off;  // local haplotype id -> offset in this chunk's pool
+    std::vector<HapKey> hap_key;    // local haplotype id -> key
+    int max_h = 0;
+    int64_t cells = 0;
+  };
+  const int nth = n >= (1 << 16) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  std::vector<Chunk> ch(nth);
+  auto pack_chunk = [&](Chunk &C) {
+    std::unordered_map<ReadKey, uint32_t, KeyHash> read_at;
+    std::unordered_map<HapKey, uint32_t, KeyHash> hap_at;
+    // the reference driver's r-major loop repeats a read for every haplotype and cycles the
+    // haplotypes: a last-read check and a small direct-mapped haplotype cache skip most hash lookups
+    ReadKey last_rk{nullptr, nullptr, nullptr, nullptr, nullptr, -1};
+    uint32_t last_roff = 0;
+    struct HapSlot {
+      const char *h = nullptr;
+      int len = -1;
+      uint32_t id = 0;
+    };
+    HapSlot hcache[256];
+    std::vector<uint8_t> &pool = C.pool;
+    for (int k = C.lo; k < C.hi; k++) {
+      const gb_testcase &t = tcs[k];
+      const ReadKey rk{t.rs, t.q, t.i, t.d, t.c, t.rslen};
+      uint32_t roff;
+      auto ri = rk == last_rk ? read_at.end() : read_at.find(rk);
+      if (rk == last_rk) {
+        roff = last_roff;
+      } else if (ri != read_at.end()) {
+        roff = ri->second;
       } else {
-        id = (uint32_t)hap_off_of.size();
-        const uint32_t hoff = (uint32_t)pool.size();
-        pool.resize(pool.size() + (size_t)t.haplen);
-        for (int c = 0; c < t.haplen; c++) pool[hoff + c] = base_code(t.hap[c]);
-        hap_at.emplace(hk, id);
-        hap_off_of.push_back(hoff);
+        roff = (uint32_t)pool.size();
+        pool.resize(pool.size() + 5 * (size_t)t.rslen);
+        uint8_t *rec = pool.data() + roff;
+        for (int r = 0; r < t.rslen; r++) {
+          rec[r] = read_match_mask(base_code(t.rs[r]));
+          rec[t.rslen + r] = (uint8_t)t.q[r];
+          rec[2 * t.rslen + r] = (uint8_t)t.i[r];
+          rec[3 * t.rslen + r] = (uint8_t)t.d[r];
+          rec[4 * t.rslen + r] = (uint8_t)t.c[r];
+        }
+        read_at.emplace(rk, roff);
       }
-      hs.h = t.hap;
-      hs.len = t.haplen;
-      hs.id = id;
+      last_rk = rk;
+      last_roff = roff;
+      const HapKey hk{t.hap, t.haplen};
+      HapSlot &hs = hcache[(((uintptr_t)t.hap) >> 4) & 255];
+      uint32_t id;
+      if (hs.h == t.hap && hs.len == t.haplen) {
+        id = hs.id;
+      } else {
+        auto hi = hap_at.find(hk);
+        if (hi != hap_at.end()) {
+          id = hi->second;
+        } else {
+          id = (uint32_t)C.hap_off.size();
+          const uint32_t hoff = (uint32_t)pool.size();
+          pool.resize(pool.size() + (size_t)t.haplen);
+          for (int c = 0; c < t.haplen; c++) pool[hoff + c] = base_code(t.hap[c]);
+          hap_at.emplace(hk, id);
+          C.hap_off.push_back(hoff);
+          C.hap_key.push_back(hk);
+        }
+        hs.h = t.hap;
+        hs.len = t.haplen;
+        hs.id = id;
+      }
+      hid[k] = id;  // local until the merge
+      desc[k].read_off = roff;  // chunk-relative until the merge
+      desc[k].dims = (uint32_t)t.rslen | ((uint32_t)t.haplen << 16);
+      desc[k].out_idx = (uint32_t)k;
+      C.max_h = std::max(C.max_h, t.haplen);
+      C.cells += (int64_t)t.rslen * t.haplen;
     }
-    const uint32_t hoff = hap_off_of[id];
-    hid[k] = id;
-    GB_ARG(pool.size() < (1ull << 32), "batch pool exceeds 4 GiB");
-    desc[k].read_off = roff;
-    desc[k].hap_off = hoff;
-    desc[k].dims = (uint32_t)t.rslen | ((uint32_t)t.haplen << 16);
-    desc[k].out_idx = (uint32_t)k;
-    max_h = std::max(max_h, t.haplen);
-    cells += (int64_t)t.rslen * t.haplen;
+  };
+  for (int t = 0; t < nth; t++) {
+    ch[t].lo = (int)((int64_t)n * t / nth);
+    ch[t].hi = (int)((int64_t)n * (t + 1) / nth);
+  }
+  if (nth == 1) {
+    pack_chunk(ch[0]);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(pack_chunk, std::ref(ch[t]));
+    pack_chunk(ch[0]);
+    for (auto &x : th) x.join();
+  }
+  // merge: chunk pool bases, global haplotype ids (first appearance), one pool
+  std::vector<size_t> base(nth + 1, 0);
+  for (int t = 0; t < nth; t++) base[t + 1] = base[t] + ch[t].pool.size();
+  GB_ARG(base[nth] < (1ull << 32), "batch pool exceeds 4 GiB");
+  std::vector<uint32_t> hap_off_of;
+  std::vector<std::vector<uint32_t>> gid(nth);
+  {
+    std::unordered_map<HapKey, uint32_t, KeyHash> hap_at;
+    for (int t = 0; t < nth; t++) {
+      gid[t].resize(ch[t].hap_off.size());
+      for (size_t h = 0; h < ch[t].hap_off.size(); h++) {
+        auto it = hap_at.find(ch[t].hap_key[h]);
+        if (it == hap_at.end()) {
+          it = hap_at.emplace(ch[t].hap_key[h], (uint32_t)hap_off_of.size()).first;
+          hap_off_of.push_back((uint32_t)(base[t] + ch[t].hap_off[h]));
+        }
+        gid[t][h] = it->second;
+      }
+    }
+  }
+  std::vector<uint8_t> pool(base[nth]);
+  int max_h = 0;
+  int64_t cells = 0;
+  for (int t = 0; t < nth; t++) {
+    max_h = std::max(max_h, ch[t].max_h);
+    cells += ch[t].cells;
+  }
+  auto merge_chunk = [&](int t) {
+    if (!ch[t].pool.empty()) std::memcpy(pool.data() + base[t], ch[t].pool.data(), ch[t].pool.size());
+    for (int k = ch[t].lo; k < ch[t].hi; k++) {
+      hid[k] = gid[t][hid[k]];
+      desc[k].read_off += (uint32_t)base[t];
+      desc[k].hap_off = hap_off_of[hid[k]];
+    }
+  };
+  if (nth == 1) {
+    merge_chunk(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(merge_chunk, t);
+    merge_chunk(0);
+    for (auto &x : th) x.join();
   }
   // Stacks (phmm_stack): testcases grouped by haplotype, stacked up to kStackRows rows (R + 2 per
   // testcase) and 64 testcases; longest-processing-time first (the dispatcher hands out workgroups
