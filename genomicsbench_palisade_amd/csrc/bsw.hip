@@ -17,11 +17,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/gb_bsw.h"
@@ -636,52 +638,94 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   GB_ARG(params->e_del > 0 && params->e_ins > 0, "gb_bsw_batch_create: gap extension must be > 0");
   GB_ARG(ref_bytes >= 0 && qer_bytes >= 0 && (ref_bytes == 0 || ref) && (qer_bytes == 0 || qer),
          "gb_bsw_batch_create: bad sequence buffers");
-  int mx = 0;
-  for (int k = 0; k < 25; ++k) mx = std::max(mx, (int)params->mat[k]);
+  int st0 = GB_OK;
+  int mx = 0, mn = 0;
+  for (int k = 0; k < 25; ++k) {
+    mx = std::max(mx, (int)params->mat[k]);
+    mn = std::min(mn, (int)params->mat[k]);
+  }
+  // The sequence buffers (the bulk of the bytes) go up on a helper thread while this one builds
+  // the launch plan; the helper is joined on every return path.
+  if ((st0 = bsw_reserve(&B->d_tgt, B->cap_tgt, (size_t)std::max<int64_t>(ref_bytes, 1)))) return st0;
+  if ((st0 = bsw_reserve(&B->d_qry, B->cap_qry, (size_t)std::max<int64_t>(qer_bytes, 1)))) return st0;
+  hipError_t up_err = hipSuccess;
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } up;
+  auto upload = [&, dev = B->device, dt = B->d_tgt, dq = B->d_qry] {
+    up_err = hipSetDevice(dev);
+    if (up_err == hipSuccess && ref_bytes) up_err = hipMemcpy(dt, ref, (size_t)ref_bytes, hipMemcpyHostToDevice);
+    if (up_err == hipSuccess && qer_bytes) up_err = hipMemcpy(dq, qer, (size_t)qer_bytes, hipMemcpyHostToDevice);
+  };
+  if (ref_bytes + qer_bytes >= (16ll << 20))
+    up.t = std::thread(upload);
+  else
+    upload();  // small calls (the reference's 512-pair batches): no thread start-up
+  // per pair: descriptor, kernel variant and sort key -- in parallel chunks for big batches; a bad
+  // pair is reported by the sequential check below (first offending index)
+  // variant: the pair-per-lane kernel needs qlen < 8*NCH (NCH <= 20) and scores that fit the 16-bit
+  // eh packing; everything else goes to the wave-per-pair kernel. Sort key: variant, then query
+  // length in steps of 4 (similar band ends per wave), then decreasing target length (similar row
+  // counts per wave).
+  constexpr int kQB = 64, kTB = 4096;
+  const bool lane_ok = params->o_del >= 0 && params->o_ins >= 0 && mn >= -128 && mx <= 127;
   std::vector<gbbsw::Pair> P((size_t)n);
-  for (int64_t p = 0; p < n; ++p) {
+  std::vector<uint8_t> var((size_t)n);
+  std::vector<uint32_t> keys((size_t)n);
+  std::atomic<int64_t> bad{n};
+  auto plan = [&](int64_t lo, int64_t hi) {
+    for (int64_t p = lo; p < hi; ++p) {
+      const gb_seqpair &s = pairs[p];
+      if (!(s.len2 >= 1 && s.len2 <= GB_BSW_MAX_QLEN && s.len1 >= 0 && s.idr >= 0 && s.idr + s.len1 <= ref_bytes &&
+            s.idq >= 0 && s.idq + s.len2 <= qer_bytes)) {
+        int64_t b = bad.load();
+        while (p < b && !bad.compare_exchange_weak(b, p)) {
+        }
+        return;
+      }
+      const gbbsw::Pair q{s.idr, s.idq, s.len1, s.len2, s.h0, gbbsw::adjust_w(params->w, s.len2, mx, *params)};
+      P[p] = q;
+      int v = 5;
+      if (lane_ok && q.h0 >= 0 && (int64_t)q.h0 + (int64_t)q.qlen * mx < 30000) {
+        const int nch = (q.qlen + 8) / 8;  // columns 0..qlen
+        v = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 12 ? 2 : nch <= 16 ? 3 : nch <= 20 ? 4 : 5;
+      }
+      var[p] = (uint8_t)v;
+      keys[p] = (uint32_t)(((size_t)v * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
+                           (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1)));
+    }
+  };
+  const int nth = n >= (1 << 17) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  if (nth == 1) {
+    plan(0, n);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(plan, n * t / nth, n * (t + 1) / nth);
+    plan(0, n / nth);
+    for (auto &x : th) x.join();
+  }
+  if (bad.load() < n) {
+    const int64_t p = bad.load();
     const gb_seqpair &s = pairs[p];
     GB_ARG(s.len2 >= 1 && s.len2 <= GB_BSW_MAX_QLEN && s.len1 >= 0,
            "gb_bsw_batch_create: pair %lld has len1=%d len2=%d (need len2 in [1,%d])", (long long)p,
            s.len1, s.len2, GB_BSW_MAX_QLEN);
-    GB_ARG(s.idr >= 0 && s.idr + s.len1 <= ref_bytes && s.idq >= 0 && s.idq + s.len2 <= qer_bytes,
-           "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
-    P[p] = {s.idr, s.idq, s.len1, s.len2, s.h0, gbbsw::adjust_w(params->w, s.len2, mx, *params)};
-  }
-  // variant per pair: the pair-per-lane kernel needs qlen < 8*NCH (NCH <= 20) and scores that fit
-  // the 16-bit eh packing; everything else goes to the wave-per-pair kernel
-  int mn = 0;
-  for (int k = 0; k < 25; ++k) mn = std::min(mn, (int)params->mat[k]);
-  std::vector<uint8_t> var((size_t)n);
-  // sort key: variant, then query length in steps of 4 (similar band ends per wave), then decreasing
-  // target length (similar row counts per wave)
-  constexpr int kQB = 64, kTB = 4096;
-  auto key = [&](int64_t p) -> size_t {
-    const gbbsw::Pair &q = P[p];
-    return ((size_t)var[p] * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
-           (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1));
-  };
-  const bool lane_ok = params->o_del >= 0 && params->o_ins >= 0 && mn >= -128 && mx <= 127;
-  for (int64_t p = 0; p < n; ++p) {
-    const gbbsw::Pair &q = P[p];
-    int v = 5;
-    if (lane_ok && q.h0 >= 0 && (int64_t)q.h0 + (int64_t)q.qlen * mx < 30000) {
-      const int nch = (q.qlen + 8) / 8;  // columns 0..qlen
-      v = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 12 ? 2 : nch <= 16 ? 3 : nch <= 20 ? 4 : 5;
-    }
-    var[p] = (uint8_t)v;
+    GB_ARG(false, "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
   }
   std::vector<uint32_t> order((size_t)n);
   {
     std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * kQB * kTB + 1, 0);
-    for (int64_t p = 0; p < n; ++p) cnt[key(p)]++;
+    for (int64_t p = 0; p < n; ++p) cnt[keys[p]]++;
     int64_t acc = 0;
     for (auto &c : cnt) {
       const int64_t t = c;
       c = acc;
       acc += t;
     }
-    for (int64_t p = 0; p < n; ++p) order[cnt[key(p)]++] = (uint32_t)p;
+    for (int64_t p = 0; p < n; ++p) order[cnt[keys[p]]++] = (uint32_t)p;
   }
   for (int v = 0; v <= gb_bsw_batch::kVariants; ++v) B->seg[v] = 0;
   for (int64_t p = 0; p < n; ++p) B->seg[var[p] + 1]++;
@@ -697,13 +741,11 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   if (!st) st = bsw_reserve(&B->d_cells, cap_cells, nn);
   if (st) return st;
   B->cap_n = std::max(B->cap_n, nn);
-  if ((st = bsw_reserve(&B->d_tgt, B->cap_tgt, (size_t)std::max<int64_t>(ref_bytes, 1)))) return st;
-  if ((st = bsw_reserve(&B->d_qry, B->cap_qry, (size_t)std::max<int64_t>(qer_bytes, 1)))) return st;
   if (n) GB_HIP(hipMemcpyAsync(B->d_order, order.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, B->stream));
   if (n) GB_HIP(hipMemcpyAsync(B->d_pairs, P.data(), (size_t)n * sizeof(gbbsw::Pair), hipMemcpyHostToDevice, B->stream));
-  if (ref_bytes) GB_HIP(hipMemcpyAsync(B->d_tgt, ref, (size_t)ref_bytes, hipMemcpyHostToDevice, B->stream));
-  if (qer_bytes) GB_HIP(hipMemcpyAsync(B->d_qry, qer, (size_t)qer_bytes, hipMemcpyHostToDevice, B->stream));
   GB_HIP(hipStreamSynchronize(B->stream));  // the host vectors die on return
+  if (up.t.joinable()) up.t.join();
+  GB_HIP(up_err);
   return GB_OK;
 }
 
@@ -855,16 +897,24 @@ int gb_bsw_batch_results(gb_bsw_batch *B, gb_seqpair *pairs, int32_t *out6, int3
       dst = o.data();
     }
     GB_HIP(hipMemcpy(dst, B->d_out6, n * 6 * sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (pairs)
-      for (size_t p = 0; p < n; ++p) {
-        const int32_t *r = dst + 6 * p;
-        pairs[p].score = r[0];
-        pairs[p].qle = r[1];
-        pairs[p].tle = r[2];
-        pairs[p].gtle = r[3];
-        pairs[p].gscore = r[4];
-        pairs[p].max_off = r[5];
-      }
+    if (pairs) {
+      auto scatter = [&](size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; ++p) {
+          const int32_t *r = dst + 6 * p;
+          pairs[p].score = r[0];
+          pairs[p].qle = r[1];
+          pairs[p].tle = r[2];
+          pairs[p].gtle = r[3];
+          pairs[p].gscore = r[4];
+          pairs[p].max_off = r[5];
+        }
+      };
+      const size_t nth = n >= (1u << 17) ? std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+      std::vector<std::thread> th;
+      for (size_t t = 1; t < nth; t++) th.emplace_back(scatter, n * t / nth, n * (t + 1) / nth);
+      scatter(0, n / nth);
+      for (auto &x : th) x.join();
+    }
   }
   if (n && cells) GB_HIP(hipMemcpy(cells, B->d_cells, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   if (total_cells) {
