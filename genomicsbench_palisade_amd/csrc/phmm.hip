@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -667,7 +668,21 @@ namespace {
 
 // Pack the testcases (deduplicated reads/haplotypes, LPT order) and upload them into b, growing its
 // device buffers when they are too small. b's stream/events exist already.
+// GB_PHMM_HOSTPROF=1: host phase times of the drop-in path on stderr (development aid)
+struct HostClock {
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  HostClock() : on(getenv("GB_PHMM_HOSTPROF") != nullptr), t0(std::chrono::steady_clock::now()) {}
+  void mark(const char *what) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[phmm host] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  }
+};
+
 int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
+  HostClock clk;
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
   // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once. Inputs are validated
   // first (sequentially, so the error names the first bad testcase), then big jobs pack in
@@ -681,6 +696,7 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
            t.haplen, kMaxHaplen);
     GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
   }
+  clk.mark("validate");
   std::vector<TcDesc> desc(n);
   std::vector<uint32_t> hid(n);  // dense haplotype index of each testcase (stack grouping)
   struct Chunk {
@@ -773,6 +789,7 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     pack_chunk(ch[0]);
     for (auto &x : th) x.join();
   }
+  clk.mark("pack");
   // merge: chunk pool bases, global haplotype ids (first appearance), one pool
   std::vector<size_t> base(nth + 1, 0);
   for (int t = 0; t < nth; t++) base[t + 1] = base[t] + ch[t].pool.size();
@@ -816,6 +833,7 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     merge_chunk(0);
     for (auto &x : th) x.join();
   }
+  clk.mark("merge");
   // Stacks (phmm_stack): testcases grouped by haplotype, stacked up to kStackRows rows (R + 2 per
   // testcase) and 64 testcases; longest-processing-time first (the dispatcher hands out workgroups
   // in grid order).
@@ -842,15 +860,21 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     stacks.push_back(S);
     scost.push_back((uint64_t)((rows + kWave - 1) / kWave) * (uint64_t)(C + kWave));
   }
-  std::vector<int> sorder(stacks.size());
-  for (size_t k = 0; k < stacks.size(); k++) sorder[k] = (int)k;
-  std::stable_sort(sorder.begin(), sorder.end(), [&](int a, int b) { return scost[a] > scost[b]; });
+  // stable counting sort by decreasing cost (at most 1026 stripes x (kMaxHaplen + 64) columns)
   std::vector<Stack> sorted_stacks(stacks.size());
-  for (size_t k = 0; k < stacks.size(); k++) sorted_stacks[k] = stacks[sorder[k]];
+  {
+    uint64_t cmax = 0;
+    for (uint64_t c : scost) cmax = std::max(cmax, c);
+    std::vector<uint32_t> at((size_t)cmax + 2, 0);
+    for (uint64_t c : scost) at[(size_t)(cmax - c) + 1]++;
+    for (size_t c = 1; c < at.size(); c++) at[c] += at[c - 1];
+    for (size_t k = 0; k < stacks.size(); k++) sorted_stacks[at[(size_t)(cmax - scost[k])]++] = stacks[k];
+  }
   std::vector<uint32_t> stk_tc(order.begin(), order.end());
   if (pool.empty()) pool.resize(4);
   pool.resize((pool.size() + 15) & ~size_t(15));
 
+  clk.mark("stacks");
   const size_t nn = std::max(n, 1);
   if (nn > b->cap_n) {
     for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
@@ -886,6 +910,7 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   }
   GB_HIP(hipMemcpyAsync(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice, b->stream));
   GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
+  clk.mark("upload");
   b->n = n;
   b->nstacks = (int)sorted_stacks.size();
   b->max_haplen = max_h;
@@ -1095,8 +1120,12 @@ int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f
   if (!b) return st;
   b->force_f64 = false;
   if ((st = batch_fill(b, tcs, n))) return st;
+  HostClock clk;
   st = gb_phmm_batch_run(b);
+  if (!st) st = gb_phmm_batch_sync(b);
+  clk.mark("kernels");
   if (!st) st = gb_phmm_batch_results(b, results, raw_f, raw_d, used_double, nullptr);
+  clk.mark("results");
   return st;
 }
 
