@@ -59,7 +59,12 @@ def pmc_traffic_detail(kernel: str):
     tools/pmc_summary.py, fetch corrected by the calibrated factor of the kernel's read class);
     None when no profile covers it. PMC cannot run inside the timed process."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    # checkpoint order is the file name (r01k < r02d < r02k < r03a ...), never mtime: on the GPU box
+    # mtimes are the push order. GB_PMC_CHECKPOINT pins one checkpoint.
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.basename)
+    pin = os.environ.get("GB_PMC_CHECKPOINT")
+    if pin:
+        files = [f for f in files if os.path.basename(f) == f"{pin}_pmc.json"]
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -134,22 +139,22 @@ def device_sync():
         pass
 
 
-def cpu_baseline_phmm(ta, sample_seconds: float):
+def cpu_baseline_phmm(ta, sample_seconds: float, gpu=None, threads=None):
     """Reference GKL kernels (oracle/_ref, kind 'reference') -- or the C restatement when the
-    reference build is absent (kind 'port') -- on a bounded random sample of the same job."""
+    reference build is absent (kind 'port') -- on a bounded random sample of the same job.
+    gpu = (results, raw f32, raw f64) of the GPU pass over `ta`: the sample's outputs are compared
+    with them bit for bit and the run fails on any mismatch."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: F401
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))  # the GPU box grants 16 CPUs per GPU
+    if threads is None:
+        threads = max(1, min(16, _cores()))  # the GPU box grants 16 CPUs per GPU
     ref = oracle_lib.ref_phmm()
     rng = np.random.default_rng(123)
     order = rng.permutation(ta.n)
     kind = "reference" if ref is not None else "port"
     engine = 512 if (ref is not None and ref.ref_phmm_has_avx512()) else 256
+    last = {}
 
     def run(sub):
         n = sub.n
@@ -161,6 +166,7 @@ def cpu_baseline_phmm(ta, sample_seconds: float):
         else:
             oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(sub.arr), n, out.ctypes.data,
                                                   rf.ctypes.data, rd.ctypes.data, None, threads)
+        last["out"] = (out, rf, rd)
         return time.perf_counter() - t0
 
     # warm the reference's static tables (Context ctors) outside the timed region, calibrate on a
@@ -178,9 +184,20 @@ def cpu_baseline_phmm(ta, sample_seconds: float):
     t = sum(run(sub) for _ in range(reps))
     gcups = reps * sub.cells() / t / 1e9
     eng = {512: "AVX-512", 256: "AVX2"}[engine] if ref is not None else "C"
-    return {"value": gcups, "unit": "GCUPS", "cores": threads, "kind": kind,
-            "sample": f"{m} of {ta.n} testcases ({sub.cells() / 1e9:.2f} G cells, random) of the same "
-                      f"job x {reps} passes, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
+    res = {"value": gcups, "unit": "GCUPS", "cores": threads, "kind": kind,
+           "sample": f"{m} of {ta.n} testcases ({sub.cells() / 1e9:.2f} G cells, random) of the same "
+                     f"job x {reps} passes, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
+    if gpu is not None:
+        sel = order[:m]
+        bad = {name: int((g[sel].view(u) != e.view(u)).sum())
+               for name, g, e, u in zip(("log10", "raw_f32", "raw_f64"), gpu, last["out"],
+                                        (np.uint64, np.uint32, np.uint64))}
+        res["parity_check"] = {"testcases": int(m), "of": int(ta.n), "mismatches": bad,
+                               "bit_exact": not any(bad.values()),
+                               "against": f"reference GKL {eng}" if ref is not None else "C restatement"}
+        if any(bad.values()):
+            raise SystemExit(f"phmm parity FAILED on the CPU-baseline sample: {res['parity_check']}")
+    return res
 
 
 def cpu_baseline_fmi(oracle_index, codes, lens, sample_seconds: float, fmi=None, idx=None):
@@ -253,27 +270,58 @@ def cpu_host():
     except OSError:
         pass
     return {"nproc": os.cpu_count(), "affinity": _cores(), "model": model,
+            "physical_cores": physical_cores(),
             "note": "cpu_baseline.cores = threads used (<= 16, the GPU box's CPU share per GPU); "
-                    "per_core = value / cores"}
+                    "per_core = value / cores; all_core_estimate = per_core x nproc "
+                    "(linear over every logical CPU, i.e. generous to the CPU: the box only grants 16 CPUs to a run)"}
 
 
-def add_per_core(obj):
-    """cpu_baseline objects (nested ones too) get value per thread used."""
+def physical_cores():
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo: the host's physical cores."""
+    seen, phys, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("physical id"):
+                    phys = ln.split(":", 1)[1].strip()
+                elif ln.startswith("core id"):
+                    core = ln.split(":", 1)[1].strip()
+                elif not ln.strip():
+                    if core is not None:
+                        seen.add((phys, core))
+                    phys = core = None
+    except OSError:
+        return None
+    if core is not None:
+        seen.add((phys, core))
+    return len(seen) or None
+
+
+def add_per_core(obj, cores_all=None):
+    """cpu_baseline objects (nested ones too) get value per thread used and the all-core estimate
+    of BASELINE.md section 3 (per thread x every logical CPU of the host: an upper bound for the CPU,
+    SMT siblings do not double a core's rate)."""
+    if cores_all is None:
+        cores_all = os.cpu_count()
     if isinstance(obj, dict):
         if "cpu_baseline" in obj and isinstance(obj["cpu_baseline"], dict):
             cb = obj["cpu_baseline"]
             if cb.get("value") and cb.get("cores"):
                 cb["per_core"] = cb["value"] / cb["cores"]
+                if cores_all:
+                    cb["all_core_estimate"] = {"value": cb["per_core"] * cores_all, "cores": cores_all}
             if isinstance(cb.get("port"), dict) and cb["port"].get("value") and cb["port"].get("cores"):
                 cb["port"]["per_core"] = cb["port"]["value"] / cb["port"]["cores"]
         for v in obj.values():
-            add_per_core(v)
+            add_per_core(v, cores_all)
 
 
-def cpu_baseline_chain(calls, sample_seconds: float):
+def cpu_baseline_chain(calls, sample_seconds: float, gpu=None):
     """The reference's scalar chain_dp (tools/minimap2-acceleration/kernel/scalar, compiled from the
     reference tree into oracle/_ref, kind 'reference'; the C restatement when absent, kind 'port')
-    over a bounded random sample of the same calls, OpenMP over calls like host_chain_kernel."""
+    over a bounded random sample of the same calls, OpenMP over calls like host_chain_kernel.
+    gpu = (scores, parents, targets, peaks) of the GPU pass over `calls`: the reference is run once
+    over every call first and its outputs compared bit for bit (the run fails on a mismatch)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from genomicsbench_palisade_amd import gen
@@ -281,6 +329,16 @@ def cpu_baseline_chain(calls, sample_seconds: float):
     ref = oracle_lib.ref_chain()
     rng = np.random.default_rng(321)
     order = rng.permutation(calls.ncalls)
+    check = None
+    if gpu is not None:
+        exp = oracle_lib.ref_chain_run(ref, calls, threads) if ref is not None else oracle_lib.chain_oracle(calls, threads)
+        bad = {name: int((np.asarray(g) != np.asarray(e)).sum())
+               for name, g, e in zip(("score", "parent", "target", "peak_score"), gpu, exp[:4])}
+        check = {"calls": int(calls.ncalls), "anchors": int(calls.nanchors), "mismatches": bad,
+                 "bit_exact": not any(bad.values()),
+                 "against": "minimap2-acceleration scalar chain_dp" if ref is not None else "C restatement"}
+        if any(bad.values()):
+            raise SystemExit(f"chain parity FAILED over the bench set: {check}")
 
     def sub(idx):
         idx = np.sort(idx)
@@ -311,14 +369,16 @@ def cpu_baseline_chain(calls, sample_seconds: float):
             "kind": "reference" if ref is not None else "port",
             "sample": f"{m} of {calls.ncalls} calls ({s_.nanchors} anchors, random) of the same set, "
                       f"{'minimap2-acceleration scalar chain_dp' if ref is not None else 'C restatement'}, "
-                      f"OpenMP {threads} threads, {reps} pass(es) of {t:.2f} s"}
+                      f"OpenMP {threads} threads, {reps} pass(es) of {t:.2f} s",
+            "parity_check": check}
 
 
-def cpu_baseline_bsw(pairs, params, sample_seconds: float):
+def cpu_baseline_bsw(pairs, params, sample_seconds: float, gpu=None):
     """bwa v1 ksw_extend2 compiled from the reference tree (oracle/_ref/libref_bwa.so) -- the function
     the benchmark's scalarBandedSWA (bandedSWA.cpp:130-251) restates; the benchmark's own SSE
     getScores16 needs Palisade and is not buildable here -- on a bounded random sample of the same
-    pairs, one pair stream per thread (ctypes releases the GIL). Falls back to the C restatement."""
+    pairs, one pair stream per thread (ctypes releases the GIL). Falls back to the C restatement.
+    gpu = out6 [n, 6] of the GPU pass over `pairs`: the sample's outputs are compared bit for bit."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from concurrent.futures import ThreadPoolExecutor
@@ -331,23 +391,36 @@ def cpu_baseline_bsw(pairs, params, sample_seconds: float):
         t0 = time.perf_counter()
         with ThreadPoolExecutor(threads) as ex:
             if ref is not None:
-                list(ex.map(lambda q: oracle_lib.ref_bsw_run(ref, q, params), parts))
+                outs = list(ex.map(lambda q: oracle_lib.ref_bsw_run(ref, q, params), parts))
             else:
-                list(ex.map(lambda q: oracle_lib.bsw_oracle(q, params, 1), parts))
-        return time.perf_counter() - t0
+                outs = list(ex.map(lambda q: oracle_lib.bsw_oracle(q, params, 1)[0], parts))
+        t = time.perf_counter() - t0
+        out6 = np.zeros((sub.n, 6), np.int32)
+        for k in range(threads):
+            out6[k::threads] = outs[k]
+        return t, out6
 
     cal = pairs.subset(rng.choice(pairs.n, 4000 * threads, replace=False))
-    rate = cal.n / max(run(cal), 1e-6)
+    rate = cal.n / max(run(cal)[0], 1e-6)
     m = int(min(pairs.n, max(cal.n, rate * sample_seconds)))
     idx = np.sort(rng.choice(pairs.n, m, replace=False))
     sub = pairs.subset(idx)
     cells = oracle_lib.bsw_oracle(sub, params, threads)[2]
-    t = run(sub)
+    t, exp = run(sub)
+    check = None
+    if gpu is not None:
+        bad = int((np.asarray(gpu)[idx] != exp).any(axis=1).sum())
+        check = {"pairs": int(m), "of": int(pairs.n), "mismatching_pairs": bad, "bit_exact": bad == 0,
+                 "fields": "score, qle, tle, gtle, gscore, max_off",
+                 "against": "bwa ksw_extend2" if ref is not None else "C restatement"}
+        if bad:
+            raise SystemExit(f"bsw parity FAILED on the CPU-baseline sample: {check}")
     return {"value": cells / t / 1e9, "unit": "GCUPS", "cores": threads,
             "kind": "reference" if ref is not None else "port", "pairs_per_s": m / t,
             "sample": f"{m} of {pairs.n} pairs (random) of the same set, "
                       f"{'bwa ksw_extend2 (tools/bwa/ksw.c)' if ref is not None else 'C restatement'}, "
-                      f"{threads} threads, {t:.1f} s"}
+                      f"{threads} threads, {t:.1f} s",
+            "parity_check": check}
 
 
 def set_seed(args, base: int, rank: int) -> int:
@@ -376,6 +449,34 @@ def shard_note(args, what: str, lo: int, hi: int, total: int, world: int) -> str
     if args.scaling == "strong":
         return f"{what} {lo}..{hi} of {total} (rank 0 shard of {world})" if world > 1 else f"all {total} {what}"
     return f"{total} {what} per rank (own seed)"
+
+
+def proxy_on(args, world: int) -> bool:
+    """The single-GPU proxy of the N-GPU strong-scaling run: on one GPU (world 1), time each shard
+    rank r of --shard-of N would get, with the same shard.py cut the N-rank run takes."""
+    return world == 1 and args.scaling == "strong" and args.shard_of > 1
+
+
+def shard_proxy(args, full_ms: float, full_value: float, unit: str, time_rank):
+    """time_rank(r) -> (ms per step, per-GPU value) for rank r's shard of an --shard-of N job.
+    Returns each shard's per-GPU throughput, the lowest one against the full-set rate, and (all
+    ranks timed) the projected N-GPU strong-scaling speedup = full-set step / slowest shard step."""
+    ranks = range(args.shard_of) if args.shard_rank < 0 else [args.shard_rank]
+    per = []
+    for r in ranks:
+        ms, value = time_rank(r)
+        per.append({"rank": r, "ms_per_step": round(ms, 4), "value": round(value, 3)})
+    low = min(p["value"] for p in per)
+    out = {"of": args.shard_of, "unit": unit + " per GPU", "ranks": per, "per_gpu_min": low,
+           "ratio_min_vs_full": low / full_value if full_value else None,
+           "note": f"1 GPU, world size 1: each rank's strong-scaling shard of the same set (shard.py) timed "
+                   f"alone, {args.steps} steps after {args.warmup} warm-up; ratio = per-GPU rate on the "
+                   f"shard / full-set rate (>= 0.94 needed for 7.5x at 8)"}
+    if len(per) == args.shard_of:
+        worst = max(p["ms_per_step"] for p in per)
+        out["projected_speedup"] = full_ms / worst
+        out["projected_efficiency"] = full_ms / worst / args.shard_of
+    return out
 
 
 def e2e_time(fn, reps: int = 2) -> float:
@@ -472,13 +573,31 @@ def bench_chain(args, D, rank, world, kind="large"):
                      "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_kernel": ms},
     }
+    if proxy_on(args, world):
+        log(f"chain {kind}: shard proxy of {args.shard_of}")
+
+        def t_rank(r):
+            sub, _ = shard.shard_calls(full, r, args.shard_of)
+            sb = chain.ChainBatch(sub)
+            for _ in range(1 + args.warmup):
+                sb.run()
+                sb.sync()
+
+            def st():
+                sb.run()
+                sb.sync()
+                return 0.0
+            el, _ = timed_steps(D, args.steps, st)
+            sb.close()
+            return el / args.steps * 1e3, sub.nanchors * args.steps / el / 1e6
+        out["shard_proxy"] = shard_proxy(args, elapsed / args.steps * 1e3, manch, "Manchors/s", t_rank)
     if kind == "large":
         out["roofline"]["traffic"] = pmc_traffic("chain_kernel")
         out["roofline"]["traffic_detail"] = pmc_traffic_detail("chain_kernel")
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            log("chain: CPU baseline")
-            cpu = cpu_baseline_chain(calls, args.cpu_seconds)
+            log("chain: CPU baseline (+ reference run over every call, bit-exact check)")
+            cpu = cpu_baseline_chain(calls, args.cpu_seconds, gpu=b.results()[:4])
         out["cpu_baseline"] = cpu
         out["backtrack"] = bench_chain_backtrack(args, D, rank, world, b, calls)
         if not args.no_e2e:
@@ -563,7 +682,7 @@ def bench_bsw(args, D, rank, world, kind="large"):
     params = bsw.default_params()
     b = bsw.BswBatch(pairs, params)
     b.run()
-    _, _, cells = b.results(want_cells=False)
+    out6, _, cells = b.results(want_cells=False)
     for _ in range(args.warmup):
         b.run()
         b.sync()
@@ -588,13 +707,32 @@ def bench_bsw(args, D, rank, world, kind="large"):
                      "frac": ach / PEAK_INT_OPS, "ops_per_cell": BSW_OPS_PER_CELL},
         "kernels_ms": {"bsw (all launches of a step)": ms},
     }
+    if proxy_on(args, world):
+        log(f"bsw {kind}: shard proxy of {args.shard_of}")
+
+        def t_rank(r):
+            sub, _ = shard.shard_pairs(full, r, args.shard_of)
+            sb = bsw.BswBatch(sub, params)
+            for _ in range(1 + args.warmup):
+                sb.run()
+                sb.sync()
+            c = sb.results(want_cells=False)[2]
+
+            def st():
+                sb.run()
+                sb.sync()
+                return 0.0
+            el, _ = timed_steps(D, args.steps, st)
+            sb.close()
+            return el / args.steps * 1e3, c * args.steps / el / 1e9
+        out["shard_proxy"] = shard_proxy(args, elapsed / args.steps * 1e3, gcups, "GCUPS", t_rank)
     if kind == "large":
         out["roofline"]["traffic"] = pmc_traffic("bsw_lane_kernel")
         out["roofline"]["traffic_detail"] = pmc_traffic_detail("bsw_lane_kernel")
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            log("bsw: CPU baseline")
-            cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds)
+            log("bsw: CPU baseline (+ bit-exact check of the sample)")
+            cpu = cpu_baseline_bsw(pairs, params, args.cpu_seconds, gpu=out6)
         out["cpu_baseline"] = cpu
         if not args.no_e2e:
             log("bsw: drop-in end to end")
@@ -631,7 +769,7 @@ def bench_phmm(args, D, rank, world, kind="large"):
     # one checked pass first (its results give the f64 share), then the warm-up steps run straight into
     # the timed ones so the GPU does not sit idle between them
     job.run()
-    _, rf, _, used, _ = job.results()
+    res, rf, rd, used, _ = job.results()
     rl = ta.np_arr["rslen"][:ta.n].astype(np.int64)
     hl = ta.np_arr["haplen"][:ta.n].astype(np.int64)
     cells_f64 = int((rl * hl)[used.astype(bool)].sum())
@@ -666,15 +804,33 @@ def bench_phmm(args, D, rank, world, kind="large"):
         "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
     }
+    if proxy_on(args, world):
+        log(f"phmm {kind}: shard proxy of {args.shard_of}")
+
+        def t_rank(r):
+            sub, _ = shard.shard_testcases(full, r, args.shard_of)
+            sj = phmm.DeviceBatch(sub)
+            for _ in range(1 + args.warmup):
+                sj.run()
+            el, _ = timed_steps(D, args.steps, sj.run, lambda: (sj.sync(), 0.0)[1])
+            c = sj.stats()[1]
+            sj.close()
+            return el / args.steps * 1e3, c * args.steps / el / 1e9
+        out["shard_proxy"] = shard_proxy(args, elapsed / args.steps * 1e3, gcups, "GCUPS", t_rank)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if kind == "large":
+            log("phmm: CPU baseline (+ bit-exact check of the sample)")
+            cpu = cpu_baseline_phmm(ta, args.cpu_seconds, gpu=(res, rf, rd))
+        else:
+            # BASELINE.json config 1: the reference on the 'small' job, single thread
+            log("phmm small: single-thread CPU reference (+ bit-exact check of the sample)")
+            cpu = cpu_baseline_phmm(ta, args.cpu_seconds, gpu=(res, rf, rd), threads=1)
+    out["cpu_baseline"] = cpu
     if kind == "large":
         r32["traffic"] = pmc_traffic("phmm_forward<float>")
         r32["traffic_detail"] = pmc_traffic_detail("phmm_forward<float>")
         r64["traffic"] = pmc_traffic("phmm_forward<double>")
-        cpu = None
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            log("phmm: CPU baseline")
-            cpu = cpu_baseline_phmm(ta, args.cpu_seconds)
-        out["cpu_baseline"] = cpu
         if not args.no_e2e:
             log("phmm: drop-in end to end")
             job.close()
@@ -721,6 +877,8 @@ def bench_fmi(args, D, rank, world):
     alg_bytes = calls * FMI_BYTES_PER_EXT + len(lens) * 151 + total * 40
     occ_bytes = calls * FMI_OCC_BYTES_PER_EXT + len(lens) * 151 + total * 40
     ach = alg_bytes / (ms * 1e-3)
+    proxy = fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, elapsed / args.steps * 1e3, mreads) \
+        if proxy_on(args, world) else None
     cpu = None
     n, _, _ = idx.info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -767,8 +925,29 @@ def bench_fmi(args, D, rank, world):
         "cpu_baseline": cpu,
         "dropin_e2e": e2e,
         "sa_lookup": sa,
+        "shard_proxy": proxy,
         "small": small,
     }
+
+
+def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full_value):
+    log(f"fmi: shard proxy of {args.shard_of}")
+
+    def t_rank(r):
+        lo, hi = shard.read_range(len(lens_all), r, args.shard_of)
+        rs = fmi.Reads(idx, codes_all[lo:hi], lens_all[lo:hi])
+        for _ in range(1 + args.warmup):
+            rs.search(19)
+            rs.sync()
+
+        def st():
+            rs.search(19)
+            rs.sync()
+            return 0.0
+        el, _ = timed_steps(D, args.steps, st)
+        rs.close()
+        return el / args.steps * 1e3, (hi - lo) * args.steps / el / 1e6
+    return shard_proxy(args, full_ms, full_value, "Mreads/s", t_rank)
 
 
 def bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref):
@@ -792,7 +971,10 @@ def bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref):
     rs.close()
     nr = hi - lo
     alg = calls[0] * FMI_BYTES_PER_EXT + nr * 151 + total * 40
-    return {"value": round(D.sum(float(nr)) * args.steps / elapsed / 1e6, 3), "unit": "Mreads/s",
+    value = D.sum(float(nr)) * args.steps / elapsed / 1e6
+    proxy = fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, elapsed / args.steps * 1e3, value) \
+        if proxy_on(args, world) else None
+    return {"value": round(value, 3), "unit": "Mreads/s", "shard_proxy": proxy,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "config": {"workload": f"fmi small: {len(lens_all)} reads x 151 bp over the large index; "
                                    + shard_note(args, "reads", lo, hi, len(lens_all), world),
@@ -885,6 +1067,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end (host arrays) timings")
+    ap.add_argument("--shard-of", type=int, default=8,
+                    help="single-GPU proxy (world size 1, strong scaling): also time the shards an N-GPU run "
+                         "would give its ranks (0 or 1 = off)")
+    ap.add_argument("--shard-rank", type=int, default=-1, help="proxy only this rank's shard (-1 = every rank)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -940,6 +1126,7 @@ def main():
             "roofline": ph["roofline"] if ph else None,
             "roofline_f64": ph["roofline_f64"] if ph else None,
             "kernels_ms": ph["kernels_ms"] if ph else None,
+            "shard_proxy": ph.get("shard_proxy") if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
             "dropin_e2e": ph.get("dropin_e2e") if ph else None,
             "fmi": fm,

@@ -118,7 +118,13 @@ struct SearchArgs {
   int32_t *ovf_n;
   int32_t *fatal;        // pass 2 overflow / list overflow
   unsigned long long *bwt_calls;
-  int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof
+  int32_t budget;        // a read still running after this many backwardExt calls is handed to the
+                         // wave-cooperative pass (smem_heavy); INT32_MAX = never
+  int32_t *heavy;        // reads handed over (capacity nreads) and their count
+  int32_t *heavy_n;
+  int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof,
+                         // 8 = per-read trace (start / end wall clock, backwardExt calls) into `trace`
+  int64_t *trace;
 };
 
 // Diagnostic phase clocks (GB_FMI_FLAGS & 4): per-wave s_memtime sums of [state machine, gather
@@ -193,6 +199,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   PEnt head{};
 
   int cap = A.cap;  // slots of the current output area (kCap, or kBigCap once promoted)
+  int kb_cur = -1;  // the big slot of the current read, if promoted
   auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
     if (nout == cap && cap == kCap) {
       // promote the read to a big slot (first pass only, rare): copy what it has and carry on there
@@ -202,6 +209,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         for (int t = 0; t < kCap; t++) big[t] = o[t];
         o = big;
         cap = kBigCap;
+        kb_cur = kb;
         A.ovf_list[kb] = rd;
       }
     }
@@ -221,6 +229,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   };
 
   const bool prof = A.flags & 4;
+  int64_t t_read = 0;
   unsigned long long p_sm = 0, p_mem = 0, p_cons = 0, p_trips = 0, p_iter = 0, p_nr_trips = 0, p_nr_clk = 0;
   // next backwardExt request; `pend` = already prepared by the previous consume step (the common
   // continuation of a forward, backward or LAST extension), which skips the state machine
@@ -229,6 +238,16 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   bool pend = false;
   while (true) {
     const unsigned long long tA = prof ? clock64() : 0;
+    if (calls_read >= (uint32_t)A.budget && st != NEXT_READ && st != DONE) {
+      // a heavy read (a few per thousand, up to ~25x the median's backwardExt calls in repeats)
+      // would hold its wave, and at the end of the grid the whole step, for its full length: drop
+      // what it did (its calls are not counted, a big slot it took is released) and hand it to
+      // smem_heavy, which spreads each backward step's independent extensions over a wave
+      if (kb_cur >= 0) A.ovf_list[kb_cur] = -1;
+      A.heavy[atomicAdd(A.heavy_n, 1)] = rd;
+      pend = false;
+      st = NEXT_READ;
+    }
     // ---- advance this lane's state machine to its next backwardExt request --------------------
     bool req = pend;
     pend = false;
@@ -261,7 +280,9 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             }
           }
           o = A.slots + (size_t)slot * A.cap;
+          if (A.flags & 8) t_read = (int64_t)wall_clock64();
           cap = A.cap;
+          kb_cur = -1;
           nout = 0;
           ovf = false;
           calls_read = 0;
@@ -446,6 +467,11 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           A.phase[3 * rd + 1] = n2;
           A.phase[3 * rd + 2] = nout - n1 - n2;
           calls += calls_read;
+          if (A.flags & 8) {
+            A.trace[3 * (size_t)rd] = t_read;
+            A.trace[3 * (size_t)rd + 1] = (int64_t)wall_clock64();
+            A.trace[3 * (size_t)rd + 2] = calls_read;
+          }
           if (ovf) atomicAdd(A.fatal, 1);  // more than kBigCap SMEMs, or the big-slot pool was exhausted
           st = NEXT_READ;
           break;
@@ -582,13 +608,254 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   }
 }
 
+// ---- heavy reads: one wave per read ------------------------------------------------------------
+// In a repeat a read's `prev` lists grow long and its backward search makes numPrev extensions per
+// position j (FMI_search.cpp:1103-1160): a few reads per thousand make 2.5-25x the median's calls.
+// Those extensions are independent of each other -- only the bookkeeping after them is sequential
+// -- so here a wave takes one read: the forward and LAST extensions run wave-uniform (every lane
+// computes the same one), each backward step extends up to 64 list entries at once, and the
+// reference's sequential scan over the results becomes ballots:
+//   * the first loop stops at the first entry f with s' >= min_intv (push) or with s' < min_intv and
+//     a long enough SMEM (emit it);
+//   * from f on, an entry with s' >= min_intv is pushed iff its s' differs from curr_s, the s' of
+//     the last push -- which is always the s' of the previous entry with s' >= min_intv (an entry
+//     not pushed had the same s' as that push), so the test is against the nearest lower such lane.
+// The lists live in LDS (reads up to kHeavyMaxLen bases). Per read the SMEM set, the per-phase
+// counts and the backwardExt count are the lane kernel's; only the order inside the read's slot
+// differs, which sort_slots makes canonical (equal (m, n) keys are identical SMEMs).
+constexpr int kHeavyMaxLen = 256;
+constexpr int kHeavyBudget = 2000;  // backwardExt calls before a lane hands its read over
+
+struct HeavyArgs {
+  DevIndex F;
+  const uint8_t *qdb;
+  const int32_t *lens;
+  int32_t stride, min_seed_len, split_len;
+  const int32_t *heavy;
+  const int32_t *heavy_n;
+  gb_smem *slots;  // kCap per read
+  gb_smem *big;
+  int32_t *counts, *phase, *ovf_list, *ovf_n, *fatal;
+  unsigned long long *bwt_calls;
+};
+
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(v >> 32), src);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
+  __shared__ PEnt La[kHeavyMaxLen + 1], Lb[kHeavyMaxLen + 1];
+  __shared__ uint8_t Q[kHeavyMaxLen];
+  const DevIndex F = A.F;
+  const int lane = threadIdx.x;
+  const uint64_t below = (1ull << lane) - 1;
+  const int nh = *(volatile const int32_t *)A.heavy_n;
+  for (int t = blockIdx.x; t < nh; t += gridDim.x) {
+    const int rd = A.heavy[t];
+    const int L = A.lens[rd];
+    for (int i = lane; i < L; i += 64) Q[i] = A.qdb[(size_t)rd * A.stride + i];
+    __syncthreads();
+    // ---- output slot (lane 0 writes; every lane keeps the same counters) ----------------------
+    gb_smem *o = A.slots + (size_t)rd * kCap;
+    int cap = kCap, nout = 0;
+    bool ovf = false;
+    uint32_t calls = 0;
+    // wave-uniform: o, cap and nout are the same in every lane (the reseed loop below reads them)
+    auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
+      if (nout == cap && cap == kCap) {
+        int kb = 0;
+        if (lane == 0) kb = atomicAdd(A.ovf_n, 1);
+        kb = __shfl(kb, 0);
+        if (kb < kMaxOvf) {
+          gb_smem *big = A.big + (size_t)kb * kBigCap;
+          if (lane == 0) {
+            for (int i = 0; i < kCap; i++) big[i] = o[i];
+            A.ovf_list[kb] = rd;
+          }
+          o = big;
+          cap = kBigCap;
+        }
+      }
+      if (nout < cap) {
+        if (lane == 0) {
+          gb_smem e;
+          e.rid = (uint32_t)rd;
+          e.m = m;
+          e.n = n;
+          e.k = k;
+          e.l = l;
+          e.s = s;
+          o[nout] = e;
+        }
+      } else {
+        ovf = true;
+      }
+      nout++;
+    };
+
+    // getSMEMsOnePosOneThread for one position (FMI_search.cpp:1015-1176); returns next_x
+    auto one_pos = [&](int x, int min_intv) -> int {
+      int next_x = x + 1;
+      int a = Q[x];
+      if (a >= 4) return next_x;
+      int64_t ck = count_of(F, a), cl = count_of(F, 3 - a), cs = count_of(F, a + 1) - ck;
+      const uint32_t cm = (uint32_t)x;
+      int numPrev = 0, j;
+      for (j = x + 1; j < L; j++) {  // forward extension, wave-uniform
+        next_x = j + 1;
+        a = Q[j];
+        if (a >= 4) break;
+        int64_t ko, lo, so;
+        bwt_ext(F, cl, ck, cs, 3 - a, ko, lo, so);
+        calls++;
+        if (so != cs) {
+          if (lane == 0) La[numPrev] = pack_ent(Ent{ck, cl, cs, cm, (uint32_t)(j - 1)});
+          numPrev++;
+        }
+        if (so < min_intv) {
+          next_x = j;
+          break;
+        }
+        ck = lo;
+        cl = ko;
+        cs = so;
+      }
+      if (cs >= min_intv) {
+        if (lane == 0) La[numPrev] = pack_ent(Ent{ck, cl, cs, cm, (uint32_t)(j - 1)});
+        numPrev++;
+      }
+      __syncthreads();
+      // backward search: list r[p] = La[numPrev - 1 - p] at first (the reversed prev array), then
+      // each step's pushes in order
+      PEnt *in = La, *out = Lb;
+      bool rev = true;
+      for (j = x - 1; j >= 0; j--) {
+        a = Q[j];
+        if (a > 3) break;
+        int numCurr = 0;
+        bool found = false;
+        int64_t carry_s = -1;
+        for (int c0 = 0; c0 < numPrev; c0 += 64) {
+          const int p = c0 + lane;
+          const bool valid = p < numPrev;
+          PEnt pe{};
+          Ent e{};
+          int64_t ko = 0, lo = 0, so = 0;
+          if (valid) {
+            pe = in[rev ? numPrev - 1 - p : p];
+            e = unpack_ent(pe);
+            bwt_ext(F, e.k, e.l, e.s, a, ko, lo, so);
+          }
+          const bool v = valid && so >= min_intv;
+          const bool em = valid && so < min_intv && (e.n - e.m + 1) >= (uint32_t)A.min_seed_len;
+          const uint64_t vm = __ballot(v);
+          if (!found) {
+            const uint64_t bm = __ballot(v || em);
+            if (bm == 0) continue;  // the first loop has not stopped yet: nothing pushed
+            found = true;
+            const int f = __builtin_ctzll(bm);
+            if (!((vm >> f) & 1)) {  // the first loop stops on an emit (lanes before f have neither)
+              PEnt fe;
+              fe.w0 = (uint64_t)shfl64((int64_t)pe.w0, f);
+              fe.w1 = (uint64_t)shfl64((int64_t)pe.w1, f);
+              const Ent ee = unpack_ent(fe);
+              emit(ee.k, ee.l, ee.s, ee.m, ee.n);
+            }
+          }
+          const uint64_t lowv = vm & below;
+          const int64_t sp = shfl64(so, lowv ? 63 - __builtin_clzll(lowv) : lane);
+          const bool push = v && so != (lowv ? sp : carry_s);
+          const uint64_t pm = __ballot(push);
+          if (push) out[numCurr + __popcll(pm & below)] = pack_ent(Ent{ko, lo, so, (uint32_t)j, e.n});
+          numCurr += __popcll(pm);
+          if (vm) carry_s = shfl64(so, 63 - __builtin_clzll(vm));
+        }
+        calls += numPrev;
+        __syncthreads();
+        PEnt *tmp = in;
+        in = out;
+        out = tmp;
+        rev = false;
+        numPrev = numCurr;
+        if (numCurr == 0) break;
+      }
+      if (numPrev != 0) {
+        const Ent e = unpack_ent(in[rev ? numPrev - 1 : 0]);
+        if ((e.n - e.m + 1) >= (uint32_t)A.min_seed_len) emit(e.k, e.l, e.s, e.m, e.n);
+      }
+      __syncthreads();
+      return next_x;
+    };
+
+    // getSMEMsAllPosOneThread (min_intv 1)
+    for (int x = 0; x < L;) x = one_pos(x, 1);
+    const int n1 = nout;
+    // reseeding (fmi.cpp:293-302) over this read's phase-1 SMEMs
+    for (int ridx = 0; ridx < n1 && ridx < cap; ridx++) {
+      int mm = 0, nn = 0, ss = 0;
+      if (lane == 0) {
+        const gb_smem e = o[ridx];
+        mm = (int)e.m;
+        nn = (int)e.n;
+        ss = (int)min<int64_t>(e.s, 1 << 30);
+      }
+      mm = __shfl(mm, 0);
+      nn = __shfl(nn, 0);
+      ss = __shfl(ss, 0);
+      const int start = mm, end = nn + 1;
+      if (!(end - start < A.split_len || ss > 10)) one_pos((end + start) >> 1, ss + 1);
+    }
+    const int n2 = nout - n1;
+    // bwtSeedStrategyAllPosOneThread (FMI_search.cpp:1243-1326), max_intv 20
+    for (int x = 0; x < L;) {
+      int next_x = x + 1;
+      int a = Q[x];
+      if (a >= 4) {
+        x = next_x;
+        continue;
+      }
+      int64_t ck = count_of(F, a), cl = count_of(F, 3 - a), cs = count_of(F, a + 1) - ck;
+      const uint32_t cm = (uint32_t)x;
+      bool done = false;
+      for (int j = x + 1; j < L; j++) {
+        next_x = j + 1;
+        a = Q[j];
+        if (a >= 4) break;
+        int64_t ko, lo, so;
+        bwt_ext(F, cl, ck, cs, 3 - a, ko, lo, so);
+        calls++;
+        ck = lo;
+        cl = ko;
+        cs = so;
+        if (cs < 20 && (uint32_t)(j - (int)cm + 1) >= (uint32_t)(A.min_seed_len + 1)) {
+          if (cs > 0) emit(ck, cl, cs, cm, (uint32_t)j);
+          x = j + 1;
+          done = true;
+          break;
+        }
+      }
+      if (!done) x = next_x;
+    }
+    if (lane == 0) {
+      A.counts[rd] = nout;
+      A.phase[3 * rd + 0] = n1;
+      A.phase[3 * rd + 1] = n2;
+      A.phase[3 * rd + 2] = nout - n1 - n2;
+      atomicAdd(A.bwt_calls, (unsigned long long)calls);
+      if (ovf) atomicAdd(A.fatal, 1);
+    }
+    __syncthreads();
+  }
+}
+
 // Reads with count <= kCap are in their pass-1 slot; the rest in the pass-2 slot at the position of
 // the read in the overflow list (ovf_pos, filled by mark_overflow).
 __global__ void mark_overflow(const int32_t *__restrict__ ovf_list, const int32_t *__restrict__ ovf_n,
                               int32_t *__restrict__ ovf_pos) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = min(*ovf_n, kMaxOvf);
-  if (t < n) ovf_pos[ovf_list[t]] = t;
+  if (t < n && ovf_list[t] >= 0) ovf_pos[ovf_list[t]] = t;  // -1: released by a read handed to smem_heavy
 }
 
 // Sort every read's slot by (m asc, n desc) (sortSMEMs / compare_smem, FMI_search.cpp:1499-1534),
@@ -657,7 +924,8 @@ struct gb_fmi_reads {
   int64_t *d_offsets = nullptr;
   gb_smem *d_out = nullptr;
   int64_t out_cap = 0;
-  int32_t *d_ctl = nullptr;  // [0] next_read pass 1, [1] overflow count, [2] fatal, [3] next_read pass 2
+  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow count, [2] fatal, [3] unused, [4] heavy reads
+  int32_t *d_heavy = nullptr;  // reads handed to smem_heavy (capacity nreads)
   int32_t *d_ovf_list = nullptr;
   int32_t *d_ovf_pos = nullptr;
   gb_smem *d_big = nullptr;
@@ -665,14 +933,17 @@ struct gb_fmi_reads {
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
   bool ran = false;
+  bool complete = false;   // every buffer allocated: only such a read set is recycled on destroy
   bool scattered = false;  // d_out holds the last search's compacted SMEMs
   int64_t total = 0;
   gbfmi::SaJob *sa = nullptr;
+  int64_t *d_trace = nullptr;  // GB_FMI_FLAGS & 8 diagnostic (3 x nreads), allocated on demand
+  size_t cap_trace = 0;
   // grow-only capacities (bytes): a destroyed read set goes back to its thread's free list with its
   // stream and buffers, and the next create reuses them (no hipMalloc / hipFree per batch)
   int device = -1;
   size_t cap_qdb = 0, cap_q4 = 0, cap_lens = 0, cap_scratch = 0, cap_slots = 0, cap_ovf_pos = 0, cap_counts = 0,
-         cap_phase = 0, cap_offsets = 0, cap_temp = 0;
+         cap_phase = 0, cap_offsets = 0, cap_temp = 0, cap_heavy = 0;
 };
 
 namespace {
@@ -785,6 +1056,15 @@ int gb_fmi_debug_pack(int64_t n, const int64_t *ent, int64_t *ent_out, const int
     gbfmi::occ32_pack_counts(cnt[3 * i], cnt[3 * i + 1], cnt[3 * i + 2], w);
     gbfmi::occ32_unpack_counts(w, cnt_out[3 * i], cnt_out[3 * i + 1], cnt_out[3 * i + 2]);
   }
+  return GB_OK;
+}
+
+int gb_fmi_debug_trace(gb_fmi_reads *R, int64_t *out) {
+  GB_ARG(R && out && R->ran, "gb_fmi_debug_trace: bad arguments");
+  GB_ARG(R->d_trace && R->cap_trace >= (size_t)R->nreads * 3 * sizeof(int64_t),
+         "gb_fmi_debug_trace: the last search ran without GB_FMI_FLAGS & 8");
+  GB_HIP(hipStreamSynchronize(R->stream));
+  GB_HIP(hipMemcpy(out, R->d_trace, (size_t)R->nreads * 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
   return GB_OK;
 }
 
@@ -945,7 +1225,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
       if (e == hipSuccess) e = hipEventCreate(&ev);
     if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&R->d_big, (size_t)gbfmi::kMaxOvf * gbfmi::kBigCap * sizeof(gb_smem));
-    if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 4 * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 8 * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&R->d_calls, 2 * sizeof(unsigned long long));
   }
   R->idx = idx;
@@ -969,6 +1249,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   reserve(&R->d_slots, &R->cap_slots, nr * gbfmi::kCap * sizeof(gb_smem));
   reserve(&R->d_ovf_pos, &R->cap_ovf_pos, nr * sizeof(int32_t));
   reserve(&R->d_counts, &R->cap_counts, nr * sizeof(int32_t));
+  reserve(&R->d_heavy, &R->cap_heavy, nr * sizeof(int32_t));
   reserve(&R->d_phase, &R->cap_phase, nr * 3 * sizeof(int32_t));
   reserve(&R->d_offsets, &R->cap_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess)
@@ -987,9 +1268,11 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_lens, lens, (size_t)num_reads * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     gb::set_error("gb_fmi_reads_create: %s", hipGetErrorString(e));
+    R->complete = false;  // a partly built read set is freed, never recycled
     gb_fmi_reads_destroy(R);
     return GB_ERR_HIP;
   }
+  R->complete = true;
   *out = R;
   return GB_OK;
 }
@@ -999,14 +1282,14 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   if (R->stream) (void)hipStreamSynchronize(R->stream);
   gbfmi::sa_job_destroy(R->sa);
   R->sa = nullptr;
-  if (R->stream && R->d_big) {  // a complete read set: keep it for the next create on this thread
+  if (R->complete) {  // a complete read set: keep it for the next create on this thread
     free_reads().push_back(R);
     return GB_OK;
   }
   for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
-                  (void *)R->d_ovf_pos, (void *)R->d_big})
+                  (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_heavy})
     (void)hipFree(p);
   for (auto ev : R->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1022,7 +1305,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   GB_HIP(hipSetDevice(R->idx->device));
   if (int st = gbfmi::ensure_occ32(R->idx, R->stream)) return st;
   GB_HIP(hipEventRecord(R->ev[0], R->stream));
-  GB_HIP(hipMemsetAsync(R->d_ctl, 0, 4 * sizeof(int32_t), R->stream));
+  GB_HIP(hipMemsetAsync(R->d_ctl, 0, 8 * sizeof(int32_t), R->stream));
   GB_HIP(hipMemsetAsync(R->d_calls, 0, 2 * sizeof(unsigned long long), R->stream));
   gbfmi::SearchArgs A;
   A.F.occ = R->idx->d_occ32;
@@ -1048,6 +1331,25 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   {
     const char *e = getenv("GB_FMI_FLAGS");
     A.flags = e ? atoi(e) : 0;
+    // GB_FMI_HEAVY: the hand-over budget in backwardExt calls (0 = never hand over)
+    const char *h = getenv("GB_FMI_HEAVY");
+    const int budget = h ? atoi(h) : gbfmi::kHeavyBudget;
+    A.budget = (budget > 0 && R->stride <= gbfmi::kHeavyMaxLen) ? budget : INT32_MAX;
+  }
+  A.heavy = R->d_heavy;
+  A.heavy_n = R->d_ctl + 4;
+  A.trace = nullptr;
+  if ((A.flags & 8) && R->nreads > 0) {
+    const size_t bytes = (size_t)R->nreads * 3 * sizeof(int64_t);
+    if (bytes > R->cap_trace) {
+      (void)hipFree(R->d_trace);
+      R->d_trace = nullptr;
+      R->cap_trace = 0;
+      GB_HIP(hipMalloc(&R->d_trace, bytes));
+      R->cap_trace = bytes;
+    }
+    GB_HIP(hipMemsetAsync(R->d_trace, 0, bytes, R->stream));
+    A.trace = R->d_trace;
   }
   if (R->nreads > 0) {
     // one pass: every read, kCap slots each; a read that outgrows them is promoted in place to a
@@ -1063,6 +1365,29 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     else
       hipLaunchKernelGGL(gbfmi::smem_search<false>, dim3(blocks), dim3(64), 0, R->stream, A);
     GB_HIP(hipGetLastError());
+    if (A.budget != INT32_MAX) {
+      gbfmi::HeavyArgs H;
+      H.F = A.F;
+      H.qdb = A.qdb;
+      H.lens = A.lens;
+      H.stride = A.stride;
+      H.min_seed_len = A.min_seed_len;
+      H.split_len = A.split_len;
+      H.heavy = A.heavy;
+      H.heavy_n = A.heavy_n;
+      H.slots = A.slots;
+      H.big = A.big;
+      H.counts = A.counts;
+      H.phase = A.phase;
+      H.ovf_list = A.ovf_list;
+      H.ovf_n = A.ovf_n;
+      H.fatal = A.fatal;
+      H.bwt_calls = A.bwt_calls;
+      // the heavy-read count is on the device: a grid of 16 waves per CU strides over the list
+      hipLaunchKernelGGL(gbfmi::smem_heavy, dim3((unsigned)std::max(1, R->lanes / 64 * 16 / 12)), dim3(64), 0,
+                         R->stream, H);
+      GB_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(gbfmi::mark_overflow, dim3((gbfmi::kMaxOvf + 255) / 256), dim3(256), 0, R->stream,
                        R->d_ovf_list, R->d_ctl + 1, R->d_ovf_pos);
     GB_HIP(hipGetLastError());

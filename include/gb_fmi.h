@@ -137,6 +137,9 @@ int gb_fmi_sa_one_step(gb_fmi_index *idx, int64_t pos, int64_t *sa_entry, int64_
  * 4) set -- out = {state machine, gather wait, consume, trips, lane state-loop iterations, trips in
  * which a lane took a new read, state-machine clocks of those trips, 0}; reset != 0 zeroes them. */
 int gb_fmi_debug_prof(uint64_t out[8], int reset);
+/* Diagnostic: after a search run with GB_FMI_FLAGS bit 3 (value 8) set, out[3 r .. 3 r + 2] = the
+ * wall clock (100 MHz) at which read r was taken and finished, and its backwardExt calls. */
+int gb_fmi_debug_trace(gb_fmi_reads *R, int64_t *out);
 
 /* Diagnostic, host only (no device work): round trips through the search's packed layouts, the
  * code the kernels run. ent: n entries of {k, l, s, m, n} (k, l, s < 2^34; m, n < 2^13) packed into

@@ -123,6 +123,31 @@ def test_overflow_second_pass(fmi):
     assert rs.timing()[2] == oi.bwt_calls()
 
 
+@pytest.mark.parametrize("budget,min_seed,rep", [("1", 19, 0.3), ("150", 19, 0.3), ("700", 19, 0.4),
+                                                  ("60", 6, 0.3), ("0", 19, 0.3)])
+def test_heavy_read_pass_exact(fmi, monkeypatch, budget, min_seed, rep):
+    """Reads the lane kernel hands over after GB_FMI_HEAVY backwardExt calls are redone by the
+    wave-cooperative smem_heavy (one wave per read, 64 prev-list extensions per backward step): with
+    small budgets most reads take that path -- including reads promoted to big slots before the
+    hand-over (min_seed_len 6) and reads longer than 64 bases' lists -- and the SMEM lists, per-batch
+    and per-phase counts and backwardExt calls stay those of the oracle. Budget 0 = never hand over."""
+    monkeypatch.setenv("GB_FMI_HEAVY", budget)
+    ref = gen.fmi_reference(400_000, seed=51, repeat_frac=rep)
+    codes, lens = gen.fmi_reads(ref, 2500, read_len=151, seed=52, sub_rate=0.03, n_rate=0.002)
+    lens = lens.copy()
+    lens[::89] = np.maximum(1, lens[::89] // 4)
+    oi = fmi_util.OracleIndex(ref)
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512, min_seed_len=min_seed)
+    idx = fmi.Index.build(ref)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(min_seed)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    assert tot == len(exp)
+    assert (bc == ebc).all() and (pc == epc).all()
+    assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
+    assert rs.timing()[2] == oi.bwt_calls()
+
+
 def test_cli_dropin(fmi, golden, tmp_path):
     """bin/fmi (CLI of benchmarks/fmi/fmi.cpp: index prefix, FASTQ, batch size, minSeedLen, threads)
     with GB_FMI_PRINT_OUTPUT=1 prints the same SMEMs and per-batch totals as bwa on the golden set."""
