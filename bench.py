@@ -53,18 +53,23 @@ BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar in
 PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
-def pmc_traffic_detail(kernel: str):
+def pmc_traffic_detail(kernel: str, leg: str = ""):
     """Per-launch HBM bytes of `kernel` from the newest committed profiles/*_pmc.json (rocprofv3
     FETCH_SIZE and WRITE_SIZE passes of this same bench configuration, tools/gpu_prof.sh +
     tools/pmc_summary.py, fetch corrected by the calibrated factor of the kernel's read class);
-    None when no profile covers it. PMC cannot run inside the timed process."""
+    None when no profile covers it. PMC cannot run inside the timed process. leg = "human": the
+    profiles/*_human_pmc.json passes of `bench.py --only fmi_human` (the same kernel on the human-scale
+    index)."""
     import glob
     # checkpoint order is the file name (r01k < r02d < r02k < r03a ...), never mtime: on the GPU box
     # mtimes are the push order. GB_PMC_CHECKPOINT pins one checkpoint.
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.basename)
+    suffix = f"_{leg}_pmc.json" if leg else "_pmc.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)), key=os.path.basename)
+    if not leg:
+        files = [f for f in files if os.path.basename(f).count("_") == 1]  # rNNx_pmc.json only
     pin = os.environ.get("GB_PMC_CHECKPOINT")
     if pin:
-        files = [f for f in files if os.path.basename(f) == f"{pin}_pmc.json"]
+        files = [f for f in files if os.path.basename(f) == f"{pin}{suffix}"]
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -79,9 +84,9 @@ def pmc_traffic_detail(kernel: str):
     return None
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, leg: str = ""):
     """roofline.traffic: corrected HBM bytes per launch (number), or None."""
-    d = pmc_traffic_detail(kernel)
+    d = pmc_traffic_detail(kernel, leg)
     return None if d is None else d["bytes"]
 
 
@@ -930,6 +935,94 @@ def bench_fmi(args, D, rank, world):
     }
 
 
+def bench_fmi_human(args, D, rank, world):
+    """fmi over a human-scale index: a 3.217 Gbp synthetic genome-like reference (+RC: n = 6.43 G BWT
+    rows, the row count of the reference's human run, fmi_output:19-24; 3.2 GB of Occ32 and 6.4 GB of
+    CP_OCC against the 'large' leg's 0.51 / 1.02 GB), built on the GPU, and --fmi-human-reads reads.
+    Same step as the 'large' leg (the fmi.cpp batch pipeline over every read). The first reads are
+    checked against the oracle run over the same CP_OCC tables, bit for bit (the run fails
+    otherwise); the oracle's time on them is the CPU number (kind 'port', C restatement)."""
+    from genomicsbench_palisade_amd import fmi, gen
+    t0 = time.perf_counter()
+    log(f"fmi human: {args.fmi_human_gbp:g} Gbp reference")
+    ref = gen.fmi_reference(int(args.fmi_human_gbp * 1e9), seed=17)
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    idx = fmi.Index.build(ref)
+    t_index = time.perf_counter() - t0
+    n, _, _ = idx.info()
+    log(f"fmi human: {n} BWT rows built in {t_index:.1f} s; generating reads")
+    codes, lens = gen.fmi_reads(ref, args.fmi_human_reads, read_len=151, seed=18)
+    del ref
+    rs = fmi.Reads(idx, codes, lens)
+    for _ in range(max(1, args.warmup)):
+        rs.search(19)
+        rs.sync()
+    _, total, _, phases = rs.results(batch_size=512, want_smems=False)
+    calls = [0]
+
+    def step():
+        rs.search(19)
+        rs.sync()
+        a, _, calls[0] = rs.timing()
+        return a
+    elapsed, ms = timed_steps(D, args.steps, step)
+    rs.close()
+    calls = calls[0]
+    nr = len(lens)
+    mreads = nr * args.steps / elapsed / 1e6
+    alg_bytes = calls * FMI_BYTES_PER_EXT + nr * 151 + total * 40
+    occ_bytes = calls * FMI_OCC_BYTES_PER_EXT + nr * 151 + total * 40
+    check = cpu = None
+    if not args.no_cpu_baseline:
+        log("fmi human: oracle check + CPU time on the first reads")
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import fmi_util
+        threads = max(1, min(16, _cores()))
+        m = min(nr, args.fmi_human_check)
+        n_, c_, s_ = idx.info()
+        oi = fmi_util.OracleIndex(adopt=(n_, c_, s_, idx.cp_occ()))
+        t1 = time.perf_counter()
+        _, ocalls, parts = oi.run_threaded(codes[:m], lens[:m], threads, collect=True)
+        t_cpu = time.perf_counter() - t1
+        oi.close()
+        r2 = fmi.Reads(idx, codes[:m], lens[:m])
+        r2.search(19)
+        sm, tot, _, _ = r2.results(batch_size=512)
+        _, _, gcalls = r2.timing()
+        r2.close()
+        exp = np.concatenate(parts) if parts else sm[:0]
+        same = tot == len(exp) and all((sm[f] == exp[f]).all() for f in ("rid", "m", "n", "k", "l", "s"))
+        check = {"reads": int(m), "smems": int(tot), "bit_exact": bool(same), "backwardExt_equal": bool(gcalls == ocalls)}
+        if not (same and gcalls == ocalls):
+            raise SystemExit(f"fmi human-scale parity FAILED on the first reads: {check}")
+        cpu = {"value": m / t_cpu / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
+               "sample": f"first {m} reads, C restatement of bwa-mem2 FMI_search over the same CP_OCC tables "
+                         f"(batches of 512 over {threads} threads), {t_cpu:.1f} s"}
+    idx.close()
+    return {
+        "value": round(mreads, 3), "unit": "Mreads/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "config": {"workload": f"fmi human-scale: {args.fmi_human_gbp:g} Gbp synthetic genome-like reference (seed 17, "
+                               f"BWT rows {n}, as fmi_output:19-24's n = 6434693835), {nr} reads x 151 bp (seed 18), "
+                               f"minSeedLen 19, batch 512; one GPU",
+                   "smems_per_read": total / max(nr, 1), "num_smem1_2_3": [int(x) for x in phases],
+                   "backwardExt_per_read": calls / max(nr, 1), "index_build_s": round(t_index, 2),
+                   "reference_gen_s": round(t_gen, 2)},
+        "roofline": {"bound": "hbm", "kernel": "smem_search", "achieved": alg_bytes / (ms * 1e-3) / 1e9,
+                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": alg_bytes / (ms * 1e-3) / PEAK_HBM,
+                     "traffic": pmc_traffic("smem_search", "human"),
+                     "traffic_detail": pmc_traffic_detail("smem_search", "human"),
+                     "algorithmic_bytes": int(alg_bytes),
+                     "note": "achieved uses the reference's 128 B (two 64-B CP_OCC lines) per backwardExt; "
+                             "achieved_occ32 the kernel's own ~35 B of one Occ32 block per extension",
+                     "occ32_bytes": int(occ_bytes), "achieved_occ32": occ_bytes / (ms * 1e-3) / 1e9,
+                     "frac_occ32": occ_bytes / (ms * 1e-3) / PEAK_HBM},
+        "kernels_ms": {"smem_search (+ heavy pass, sort)": ms},
+        "parity_check": check,
+        "cpu_baseline": cpu,
+    }
+
+
 def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full_value):
     log(f"fmi: shard proxy of {args.shard_of}")
 
@@ -1061,8 +1154,12 @@ def main():
     ap.add_argument("--fmi-reads", type=int, default=10_000_000, help="fmi 'large' reads in the set")
     ap.add_argument("--fmi-small-reads", type=int, default=1_000_000, help="fmi 'small' reads in the set")
     ap.add_argument("--fmi-ref-mbp", type=float, default=512.0)
+    ap.add_argument("--fmi-human-gbp", type=float, default=3.217,
+                    help="fmi human-scale leg: reference length in Gbp (one GPU only; 0 = off)")
+    ap.add_argument("--fmi-human-reads", type=int, default=4_000_000)
+    ap.add_argument("--fmi-human-check", type=int, default=20_000, help="human-scale reads checked vs the oracle")
     ap.add_argument("--bsw-pairs", type=int, default=10_606_460, help="bsw pairs in the 'large' set")
-    ap.add_argument("--only", default=None, help="comma list of legs: phmm,fmi,chain,bsw (default all)")
+    ap.add_argument("--only", default=None, help="comma list of legs: phmm,fmi,chain,bsw,fmi_human (default all)")
     ap.add_argument("--no-small", action="store_true", help="skip the 'small'-set legs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1082,7 +1179,7 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     gb.set_device(local % ndev)
 
-    legs = set((args.only or "phmm,fmi,chain,bsw").split(","))
+    legs = set((args.only or "phmm,fmi,chain,bsw,fmi_human").split(","))
     ph = bench_phmm(args, D, rank, world) if "phmm" in legs else None
     fm = bench_fmi(args, D, rank, world) if "fmi" in legs else None
     ch = bench_chain(args, D, rank, world) if "chain" in legs else None
@@ -1100,6 +1197,10 @@ def main():
             small["bsw"] = bench_bsw(args, D, rank, world, kind="small")
     elif fm is not None:
         fm.pop("small", None)
+    if "fmi_human" in legs and world == 1 and args.fmi_human_gbp > 0:
+        hu = bench_fmi_human(args, D, rank, world)
+        fm = fm if fm is not None else {}
+        fm["human"] = hu
 
     if rank == 0:
         seeds = "seed" if args.scaling == "strong" else "seed + rank"

@@ -739,7 +739,11 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   if (!st) st = bsw_reserve(&B->d_order, cap_order, nn);
   if (!st) st = bsw_reserve(&B->d_out6, cap_out, nn * 6);
   if (!st) st = bsw_reserve(&B->d_cells, cap_cells, nn);
-  if (st) return st;
+  if (st) {
+    // one of the four shares cap_n and may now be freed or smaller: the next fill reallocates all
+    B->cap_n = 0;
+    return st;
+  }
   B->cap_n = std::max(B->cap_n, nn);
   if (n) GB_HIP(hipMemcpyAsync(B->d_order, order.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, B->stream));
   if (n) GB_HIP(hipMemcpyAsync(B->d_pairs, P.data(), (size_t)n * sizeof(gbbsw::Pair), hipMemcpyHostToDevice, B->stream));

@@ -150,22 +150,26 @@ __global__ __launch_bounds__(64) void peak_init(SplitArgs A, int32_t *link, int3
 // the position's bits above the ring size, so positions that share a slot are told apart; a mark
 // that would overwrite another mark of the same anchor at a different position (the ring is
 // smaller than max_iter) is a conflict, and the anchor is not verified (it goes to the fix-up).
+template <int RING>
 __device__ __forceinline__ uint32_t ring_tag(int k, int32_t pos) {
-  return (uint32_t)(k + 1) | ((uint32_t)pos >> 10 << 7);
+  constexpr int kLog = RING == 1024 ? 10 : 13;
+  static_assert(RING == (1 << kLog), "ring sizes: 1024 (tagged, may clash) or 8192 (> any window)");
+  return (uint32_t)(k + 1) | ((uint32_t)pos >> kLog << 7);
 }
 
+template <int RING>
 __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, int32_t jtop, int32_t st, int k,
                                                int lane, int32_t neg_lane, uint32_t *S, int32_t &M, int32_t &J,
                                                int32_t &N, uint32_t &vis, bool &conflict, int32_t *tgt, int32_t i) {
   const bool writer = ok & (pj >= st);
-  const uint32_t slot = writer ? (uint32_t)(pj & (kTagRing - 1)) : (uint32_t)(kTagRing + lane);
-  const uint32_t tw = ring_tag(k, pj);
+  const uint32_t slot = writer ? (uint32_t)(pj & (RING - 1)) : (uint32_t)(RING + lane);
+  const uint32_t tw = ring_tag<RING>(k, pj);
   const uint32_t prev = S[slot];
   conflict |= writer & ((prev & 127u) == (uint32_t)(k + 1)) & (prev != tw);
   S[slot] = tw;
   conflict |= writer & (S[slot] != tw);
   const int32_t j = jtop - lane;
-  const bool tg = S[j & (kTagRing - 1)] == ring_tag(k, j);
+  const bool tg = S[j & (RING - 1)] == ring_tag<RING>(k, j);
   const int32_t mx = scan_max(sc);
   const int32_t before = max(dpp_shr_i32(mx, INT_MIN), M);
   const bool upd = sc > before;
@@ -196,9 +200,14 @@ __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, 
 // fail[sc] = the first i whose loop does not give its own guess. The loops also write their
 // targets marks into t2 and count visited pairs per call: a call that passes in the first round has
 // all of them right; one that ever failed is re-marked after convergence (CHECK false, front = c1).
-template <bool CHECK>
+// The check pass stamps into the 1 K tagged ring: a window wider than the ring can make an anchor's
+// mark overwrite its own earlier one (a clash), which fails the anchor. The re-mark pass (whose
+// marks and visited counts are final) uses an 8 K ring, wider than any window (max_iter 5000 + 64
+// lanes), so no mark is ever lost there.
+template <bool CHECK, int RING = CHECK ? kTagRing : 8192>
 __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
-  __shared__ uint32_t S[kTagRing + 64];
+  static_assert(CHECK || RING > kMaxIter + 64, "the re-mark ring must hold any window");
+  __shared__ uint32_t S[RING + 64];
   const Chunk ch = A.chunks[blockIdx.x];
   const SplitCall Sc = A.split[ch.sc];
   const int lane = threadIdx.x;
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
   const uint64_t *X = A.x + Sc.off, *Y = A.y + Sc.off;
   const int32_t *score = A.score + Sc.off, *parent = A.parent + Sc.off;
   int32_t *tgt = A.t2 + Sc.off;
-  for (int t = lane; t < kTagRing + 64; t += 64) S[t] = 0;
+  for (int t = lane; t < RING + 64; t += 64) S[t] = 0;
   // window: lane l = anchor start-1-l; the chunk's anchors: lane l = start+l
   const int32_t j0 = start - 1 - lane;
   uint64_t wx = 0, wy = 0;
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
       const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
       int32_t M = (int32_t)(yi >> 32 & 0xff), J = -1, N = 0;
       bool conflict = false;
-      bool broke = resolve_tagged(ok ? sg + wf : INT_MIN, ok, wp, i - 1, st, k, lane, neg_lane, S, M, J, N,
+      bool broke = resolve_tagged<RING>(ok ? sg + wf : INT_MIN, ok, wp, i - 1, st, k, lane, neg_lane, S, M, J, N,
                                         vis, conflict, tgt, i);
       for (int32_t jt = i - 65; !broke && jt >= st; jt -= 64) {  // older candidates from memory
         const int32_t jj = jt - lane;
@@ -255,7 +264,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
         }
         int32_t sgo;
         const bool oko = geometry(xi, yi, xj, yj, v, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sgo);
-        broke = resolve_tagged(oko ? sgo + fj : INT_MIN, oko, pj, jt, st, k, lane, neg_lane, S, M, J, N, vis,
+        broke = resolve_tagged<RING>(oko ? sgo + fj : INT_MIN, oko, pj, jt, st, k, lane, neg_lane, S, M, J, N, vis,
                                      conflict, tgt, i);
       }
       const bool clash = __builtin_amdgcn_ballot_w64(conflict) != 0;

@@ -637,6 +637,7 @@ struct HeavyArgs {
   gb_smem *big;
   int32_t *counts, *phase, *ovf_list, *ovf_n, *fatal;
   unsigned long long *bwt_calls;
+  int64_t *trace;  // GB_FMI_FLAGS & 8 (as SearchArgs::trace), or null
 };
 
 __device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
@@ -654,6 +655,7 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
   for (int t = blockIdx.x; t < nh; t += gridDim.x) {
     const int rd = A.heavy[t];
     const int L = A.lens[rd];
+    const int64_t t_read = A.trace ? (int64_t)wall_clock64() : 0;
     for (int i = lane; i < L; i += 64) Q[i] = A.qdb[(size_t)rd * A.stride + i];
     __syncthreads();
     // ---- output slot (lane 0 writes; every lane keeps the same counters) ----------------------
@@ -844,6 +846,11 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
       A.phase[3 * rd + 2] = nout - n1 - n2;
       atomicAdd(A.bwt_calls, (unsigned long long)calls);
       if (ovf) atomicAdd(A.fatal, 1);
+      if (A.trace) {
+        A.trace[3 * (size_t)rd] = t_read;
+        A.trace[3 * (size_t)rd + 1] = (int64_t)wall_clock64();
+        A.trace[3 * (size_t)rd + 2] = -(int64_t)calls;  // negative: done by smem_heavy
+      }
     }
     __syncthreads();
   }
@@ -1383,6 +1390,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
       H.ovf_n = A.ovf_n;
       H.fatal = A.fatal;
       H.bwt_calls = A.bwt_calls;
+      H.trace = A.trace;
       // the heavy-read count is on the device: a grid of 16 waves per CU strides over the list
       hipLaunchKernelGGL(gbfmi::smem_heavy, dim3((unsigned)std::max(1, R->lanes / 64 * 16 / 12)), dim3(64), 0,
                          R->stream, H);

@@ -1,5 +1,6 @@
 // fmi_dropin.cpp -- class FMI_search (tools/bwa-mem2/src/FMI_search.h:101-224, plain build) over the C
-// ABI of csrc/fmi*.hip, so benchmarks/fmi/fmi.cpp relinks unchanged against libgb_fmi_dropin.so.
+// ABI of csrc/fmi*.hip, so a plain (non-HE) build of benchmarks/fmi/fmi.cpp links against
+// libgb_fmi_dropin.so (the shipped fmi.cpp is the HE build; see include/gb_compat/FMI_search.h).
 // Every SMEM and SA method runs on the GPU that holds the index; each returns exactly what the
 // reference writes, in the reference's order, including its caller-visible side effects on the
 // input arrays (query_pos_array of OnePos, the in-place compaction of rid/min_intv by AllPos).

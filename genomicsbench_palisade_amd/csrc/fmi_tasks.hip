@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/gb.h"
@@ -305,9 +306,17 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   A.min_seed_len = min_seed_len;
   A.maxlen = maxlen;
 
-  // the whole task set, then the overflowing subset with a slot sized to its largest count
-  std::vector<int32_t> todo(ntasks);
-  for (int32_t t = 0; t < ntasks; t++) todo[t] = t;
+  // Tiles of at most ~256 MB of `prev` scratch ((maxlen + 1) entries per task): the per-thread
+  // workspace stays bounded whatever the batch. Per tile: the whole tile, then its overflowing
+  // subset with a slot sized to its largest count.
+  int64_t tile = std::max<int64_t>(64, ((256ll << 20) / ((int64_t)(maxlen + 1) * (int64_t)sizeof(TEnt))) & ~63ll);
+  if (const char *te = getenv("GB_FMI_TASK_TILE")) tile = std::max(1, atoi(te));  // tests: force many tiles
+  bool uploaded = false;
+  int64_t calls_sum = 0;
+  for (int32_t t0 = 0; t0 < ntasks; t0 = (int32_t)std::min<int64_t>(ntasks, t0 + tile)) {
+  const int32_t t1 = (int32_t)std::min<int64_t>(ntasks, t0 + tile);
+  std::vector<int32_t> todo(t1 - t0);
+  for (int32_t t = t0; t < t1; t++) todo[t - t0] = t;
   int32_t cap = mode == kLast ? 48 : 32;
   for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
     const int32_t n = (int32_t)todo.size();
@@ -344,12 +353,13 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     A.ntasks = n;
     A.cap = cap;
     hipStream_t s = W.stream;
-    if (pass == 0) {
+    if (!uploaded) {
       GB_HIP(hipMemcpyAsync(W.buf[0], qdb, (size_t)extent, hipMemcpyHostToDevice, s));
       GB_HIP(hipMemcpyAsync(W.buf[1], lens, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
       GB_HIP(hipMemcpyAsync(W.buf[2], offs, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
-      GB_HIP(hipMemsetAsync(W.buf[9], 0, sizeof(unsigned long long), s));
+      uploaded = true;  // buffers 0-2 keep their size (and contents) for the later tiles
     }
+    if (pass == 0) GB_HIP(hipMemsetAsync(W.buf[9], 0, sizeof(unsigned long long), s));
     GB_HIP(hipMemcpyAsync(W.buf[3], rid.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     GB_HIP(hipMemcpyAsync(W.buf[4], qpos.data(), sizeof(int16_t) * n, hipMemcpyHostToDevice, s));
     GB_HIP(hipMemcpyAsync(W.buf[5], intv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
@@ -370,7 +380,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     unsigned long long calls = 0;
     if (pass == 0) GB_HIP(hipMemcpyAsync(&calls, A.calls, sizeof(calls), hipMemcpyDeviceToHost, s));
     GB_HIP(hipStreamSynchronize(s));
-    if (pass == 0 && calls_out) *calls_out = (int64_t)calls;
+    if (pass == 0) calls_sum += (int64_t)calls;
     std::vector<int32_t> again;
     int32_t need = 0;
     for (int32_t i = 0; i < n; i++) {
@@ -388,6 +398,8 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     cap = need;
   }
   GB_ARG(todo.empty(), "FMI_search: SMEM output of %zu tasks could not be sized", todo.size());
+  }
+  if (calls_out) *calls_out = calls_sum;
   return GB_OK;
 }
 

@@ -1,6 +1,9 @@
 /*
  * gb_compat/FMI_search.h -- source-compatible declaration of bwa-mem2's FMI_search class for
- * relinking benchmarks/fmi (plain, non-HE build) against the MI355X implementation.
+ * building a plain (non-HE) variant of benchmarks/fmi/fmi.cpp against the MI355X implementation.
+ * The shipped fmi.cpp is the HE build (it calls decrypt_ciphertext_to_plaintext_vector and reads
+ * seqs[].enc_seq), so it does not compile against this header as is; tests/cpp/fmi_class_driver.cpp
+ * is the plain variant (fmi.cpp's batch loop with the plaintext fields).
  *
  * Mirrors (written here, not copied):
  *   bseq1_t                          tools/bwa-mem2/src/bwa.h:60-69 (plain fields; methods read l_seq)
@@ -29,10 +32,14 @@
 #define PATH_MAX 4096
 #endif
 
+/* The plain bseq1_t. The reference's bwa.h:60-69 is the HE build's: it also carries five vecCT
+ * members, so its stride differs and an object compiled against it must not call these methods --
+ * the caller is a plain (non-HE) fmi.cpp compiled against this header. */
 typedef struct {
   int l_seq, id;
   char *name, *comment, *seq, *qual, *sam;
 } bseq1_t;
+static_assert(sizeof(bseq1_t) == 2 * sizeof(int) + 5 * sizeof(char *), "plain bseq1_t (no HE vecCT members)");
 
 typedef struct smem_struct {
   uint32_t rid;

@@ -166,3 +166,30 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault):
     b.run()  # re-run on the same buffers
     assert_same(b.results(), exp)
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split,fault", [("512,64", 53), ("1024,0", 211)])
+def test_gpu_split_remark_wide_windows(monkeypatch, split, fault):
+    """Calls whose windows hold up to max_iter (5000) anchors and whose parent links reach far back,
+    with injected wrong guesses: every split call fails at least once, so its targets marks and
+    visited counts come from the re-mark pass, whose stamp ring must hold a whole window (a 1 K ring
+    lets an anchor's mark overwrite its own earlier one). Targets and visited are asserted with the
+    scores, parents and peaks."""
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    rng = np.random.default_rng(91)
+    calls = _concat_calls([_cloud_call(rng, 14000, 24, 2000, (0, 1), 40),
+                           _cloud_call(rng, 8000, 3, 100, (0, 3), 2),
+                           _cloud_call(rng, 6000, 40, 4000, (0, 1), 200)])
+    exp = oracle_lib.chain_oracle(calls, 8)
+    monkeypatch.setenv("GB_CHAIN_SPLIT", split)
+    monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
+    ns, rounds, fixups = b.split_stats()
+    assert ns == calls.ncalls and fixups >= ns and rounds > 1
+    b.close()

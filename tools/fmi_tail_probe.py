@@ -44,8 +44,15 @@ for name, (lo, hi) in [("shard0", shard.read_range(nreads, 0, of)), ("full", (0,
     L.gb_fmi_debug_trace(rs.h, tr.ctypes.data)
     tr = tr.reshape(-1, 3)
     rs.close()
+    hv = tr[:, 2] < 0  # reads redone by smem_heavy (calls negated)
+    tr[:, 2] = np.abs(tr[:, 2])
     t_lo = tr[:, 0].min()
     st, en, c = tr[:, 0] - t_lo, tr[:, 1] - t_lo, tr[:, 2]
+    if hv.any():
+        print(f"  {int(hv.sum())} reads handed to smem_heavy: start {st[hv].min() * 1e-5:.2f} ms, end "
+              f"{en[hv].max() * 1e-5:.2f} ms, ext p50 {np.percentile(c[hv], 50):.0f} max {c[hv].max()}, "
+              f"read ms max {(en[hv] - st[hv]).max() * 1e-5:.2f}; lane-kernel reads end by "
+              f"{en[~hv].max() * 1e-5:.2f} ms", flush=True)
     span = en.max()
     # reads in flight over time (10 us bins)
     nb = int(span // 1000) + 1
@@ -65,6 +72,8 @@ for name, (lo, hi) in [("shard0", shard.read_range(nreads, 0, of)), ("full", (0,
           f"max {dur.max():.2f}; ext p50 {np.percentile(c, 50):.0f} p99 {np.percentile(c, 99):.0f} max {c.max()}; "
           f"slowest-ending read: start {st[k] * 1e-5:.2f} ms, {dur[k]:.2f} ms, {c[k]} ext", flush=True)
     if name == "shard0":
-        out = dict(st=st.astype(np.int32), en=en.astype(np.int32), calls=c.astype(np.int32))
+        out = dict(st=st.astype(np.int32), en=en.astype(np.int32), calls=c.astype(np.int32), heavy=hv)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"fmi_tail_{tag}.npz"), **out)
+import resource  # noqa: E402
+print(f"max RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB", flush=True)
