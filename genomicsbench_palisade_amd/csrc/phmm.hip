@@ -651,6 +651,7 @@ struct gb_phmm_batch {
   int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
+  int cus = 256;                   // compute units of the device (stack height rule)
   bool ran = false;
   bool force_f64 = false;
 };
@@ -846,13 +847,23 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   }
   std::vector<Stack> stacks;
   std::vector<uint64_t> scost;
+  // Stack height adapts to the job: tall stacks waste the least on partial stripes, but a job of
+  // fewer than ~4 stacks per resident wave (32 per CU) leaves the grid's tail -- one whole stack --
+  // exposed, and the f64 pass's persistent grid balances finer pieces better. Measured on the 'large'
+  // job's 1/8 strong-scaling shard (tools/phmm_shard_probe.py): 2048 rows 4.97 ms, 1024 4.51, 512 4.37,
+  // 256 4.64 per step; on the whole job 2048 rows stay best (33.0 ms; 512: 33.7).
+  int64_t total_rows = 0;
+  for (int k = 0; k < n; k++) total_rows += (int64_t)(desc[k].dims & 0xffff) + 2;
+  int stack_rows = kStackRows;
+  while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
+  if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
   for (int k = 0; k < n;) {
     const uint32_t h = desc[order[k]].hap_off;
     const int C = (int)(desc[order[k]].dims >> 16);
     Stack S{(uint32_t)k, 0, h, (uint32_t)C};
     int rows = 0;
     while (k < n && desc[order[k]].hap_off == h && S.count < (uint32_t)kWave &&
-           (S.count == 0 || rows + (int)(desc[order[k]].dims & 0xffff) + 2 <= kStackRows)) {
+           (S.count == 0 || rows + (int)(desc[order[k]].dims & 0xffff) + 2 <= stack_rows)) {
       rows += (int)(desc[order[k]].dims & 0xffff) + 2;
       S.count++;
       k++;
@@ -926,6 +937,7 @@ int batch_new(DeviceTables *tabs, gb_phmm_batch **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, tabs->device) == hipSuccess) cus = prop.multiProcessorCount;
   b->f64_grid = cus * 16;
+  b->cus = cus;
   hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
   for (auto &ev : b->ev)
     if (e == hipSuccess) e = hipEventCreate(&ev);

@@ -1,0 +1,37 @@
+"""phmm strong-scaling shard probe: the 'large' job (64 batches, seed 1) and its shard PHMM_RANK (default
+0) of PHMM_OF (default 8): per step the f32 kernel, f64 fallback and whole-step times (HIP events) and
+the sync'd wall time, with the stack count and the GB_PHMM_STACK_ROWS setting in use."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from genomicsbench_palisade_amd import gen, phmm, set_device, shard  # noqa: E402
+from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: E402
+
+set_device(0)
+phmm.init_pairhmm()
+full = TestcaseArray.from_batches(gen.phmm_dataset("large", int(os.environ.get("PHMM_BATCHES", "64")), seed=1))
+of, r = int(os.environ.get("PHMM_OF", "8")), int(os.environ.get("PHMM_RANK", "0"))
+for name, ta in [("full", full), (f"shard {r}/{of}", shard.shard_testcases(full, r, of)[0])]:
+    for rows in os.environ.get("PHMM_ROWS", "default").split(";"):
+        if rows == "default":
+            os.environ.pop("GB_PHMM_STACK_ROWS", None)
+        else:
+            os.environ["GB_PHMM_STACK_ROWS"] = rows
+        job = phmm.DeviceBatch(ta)
+        for _ in range(3):
+            job.run()
+        job.sync()
+        steps = 10
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            job.run()
+        job.sync()
+        wall = (time.perf_counter() - t0) / steps * 1e3
+        a, b, c = job.timing()
+        ntc, cells, nf64 = job.stats()
+        job.close()
+        print(f"{name:12s} rows {rows:8s}: {ntc} testcases, {cells / 1e9:.2f} G cells, f64 {nf64}; wall {wall:.3f} ms "
+              f"({cells / wall / 1e6:.1f} GCUPS); f32 {a:.3f} ms, f64 {b:.3f} ms, step {c:.3f} ms", flush=True)
