@@ -19,7 +19,8 @@ HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
 .PHONY: all ref clean oracle
 DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so $(LIB)/libgb_fmi_dropin.so
-all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle tests/_build/fmi_class_driver
+all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle tests/_build/fmi_class_driver \
+     tests/_build/libdropin_bench.so
 
 $(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIB)/obj
@@ -61,6 +62,11 @@ $(BIN)/phmm: $(PKG)/drivers/phmm_main.cpp $(LIB)/libgb.so
 tests/_build/fmi_class_driver: tests/cpp/fmi_class_driver.cpp $(LIB)/libgb_fmi_dropin.so include/gb_compat/FMI_search.h
 	@mkdir -p tests/_build
 	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(LIB) -lgb_fmi_dropin -lgb -Wl,-rpath,'$$ORIGIN/../../$(LIB)'
+
+# bench harness: host_chain_kernel / getScores16 called the way the reference benchmarks call them
+tests/_build/libdropin_bench.so: tests/cpp/dropin_bench.cpp $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so $(wildcard include/gb_compat/*.h)
+	@mkdir -p tests/_build
+	$(HOSTCXX) $(HOSTFLAGS) -pthread -shared -o $@ $< -L$(LIB) -lgb_chain_dropin -lgb_bsw_dropin -lgb -Wl,-rpath,'$$ORIGIN/../../$(LIB)'
 
 oracle:
 	$(MAKE) -s -C oracle all

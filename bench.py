@@ -516,8 +516,45 @@ def phmm_dropin_e2e(args, D, ta, cells, rank, world):
     D.barrier()
     t = D.max(e2e_time(lambda: both(ctypes.addressof(ta.arr), out.ctypes.data, ta.n)))
     res = {"computelikelihoodsboth": {"value": D.sum(float(cells)) / t / 1e9, "unit": "GCUPS", "seconds": t,
-                                      "note": "host testcase[] in, double[] out: pack + H2D + kernels + D2H + log10"}}
+                                      "note": "one call over the rank's whole job: host testcase[] in, double[] out "
+                                              "(pack + H2D + kernels + D2H + log10)"}}
     return res
+
+
+def phmm_dropin_per_batch(args, D, batches, rank, world, kernel_gcups, job_results=None):
+    """computelikelihoodsboth called once per batch, as the reference's driver does
+    (PairHMMUnitTest.cpp:549-593: one call per read_batch, batch_size = R x H <= MAX_BATCH_SIZE); the
+    rank takes a contiguous range of whole batches balanced by cells. On one GPU the calls' results are
+    checked bit for bit against the device job's results of the same testcases (job_results: the same
+    kernels, so a difference is a host-side packing error)."""
+    from genomicsbench_palisade_amd import shard
+    from genomicsbench_palisade_amd._tc import TestcaseArray
+    lib = ctypes.CDLL(os.path.join(ROOT, "genomicsbench_palisade_amd", "lib", "libgkl_pairhmm_c.so"))
+    both = getattr(lib, "_Z22computelikelihoodsbothP8testcasePdi")
+    both.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lo, hi = shard.rank_range([b.cells() for b in batches], rank, world)
+    arrs = [TestcaseArray.from_batch(b) for b in batches[lo:hi]]  # testcase[] built outside the clock
+    outs = [np.zeros(max(a.n, 1)) for a in arrs]
+    cells = float(sum(a.cells() for a in arrs))
+
+    def once():
+        for a, o in zip(arrs, outs):
+            both(ctypes.addressof(a.arr), o.ctypes.data, a.n)
+    D.barrier()
+    t = D.max(e2e_time(once))
+    value = D.sum(cells) / t / 1e9
+    check = None
+    if job_results is not None and lo == 0 and hi == len(batches):
+        got = np.concatenate([o[:a.n] for a, o in zip(arrs, outs)])
+        bad = int((got.view(np.uint64) != np.asarray(job_results).view(np.uint64)).sum())
+        check = {"testcases": int(len(got)), "mismatches": bad, "bit_exact": bad == 0,
+                 "against": "the device job's results (themselves checked against the reference GKL)"}
+        if bad:
+            raise SystemExit(f"phmm per-batch drop-in parity FAILED: {check}")
+    return {"value": value, "unit": "GCUPS", "seconds": t, "calls": hi - lo, "parity_check": check,
+            "vs_kernel_rate": value / kernel_gcups if kernel_gcups else None,
+            "note": f"computelikelihoodsboth once per batch ({hi - lo} calls of R x H testcases, batches {lo}..{hi}), "
+                    f"as PairHMMUnitTest.cpp:549-593; testcase[] prepared outside the clock"}
 
 
 def phmm_cli_e2e(batches, cells):
@@ -539,7 +576,8 @@ def phmm_cli_e2e(batches, cells):
     kr = rt[0] if rt else float("nan")
     return {"value": cells / kr / 1e9 if kr > 0 else None, "unit": "GCUPS", "kernel_runtime_s": kr, "wall_s": wall,
             "wall_gcups": cells / wall / 1e9,
-            "note": "bin/phmm on the job written as a .in file: 'Kernel runtime' (pack, H2D, kernels, D2H) and "
+            "note": "bin/phmm on the job written as a .in file: 'Kernel runtime' (the reference's timed region, "
+                    "PairHMMUnitTest.cpp:549-593: testcase construction, pack, H2D, kernels, D2H) and "
                     "process wall time (file parsing + runtime start-up included)"}
 
 
@@ -619,8 +657,51 @@ def bench_chain(args, D, rank, world, kind="large"):
                 "value": anchors_all / t / 1e6, "unit": "Manchors/s", "seconds": t,
                 "note": "host_chain_kernel's C ABI over the rank's calls in CSR: H2D + chain_dp + D2H of "
                         "score/parent/target/peak (the C++ drop-in adds the std::vector copies)"}}
+            log("chain: host_chain_kernel over std::vector (the reference's call)")
+            out["dropin_e2e"]["host_chain_kernel"] = chain_vector_e2e(D, calls, b, manch)
     b.close()
     return out
+
+
+def dropin_bench_lib():
+    """tests/_build/libdropin_bench.so: the C++ drop-ins called the way the reference drivers call them
+    (tests/cpp/dropin_bench.cpp); None when not built."""
+    path = os.path.join(ROOT, "tests", "_build", "libdropin_bench.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    lib.bench_host_chain_kernel.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
+    lib.bench_host_chain_kernel.restype = ctypes.c_double
+    lib.bench_bsw_batches.argtypes = [vp, vp, i64, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.bench_bsw_batches.restype = ctypes.c_double
+    return lib
+
+
+def chain_vector_e2e(D, calls, b, kernel_manch):
+    """host_chain_kernel(std::vector<call_t>&, std::vector<return_t>&, int) of libgb_chain_dropin.so, one
+    call over the rank's calls, timed around the call only as the reference's main.cpp:80-91 does; the
+    outputs are compared with the device batch's (bit for bit)."""
+    lib = dropin_bench_lib()
+    if lib is None:
+        return None
+    outs = [np.zeros(max(calls.nanchors, 1), np.int32) for _ in range(4)]
+    ts = []
+    for _ in range(3):
+        ts.append(lib.bench_host_chain_kernel(calls.ncalls, calls.offsets.ctypes.data, calls.avg_qspan.ctypes.data,
+                                              calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data,
+                                              16, *[o.ctypes.data for o in outs]))
+    t = D.max(float(np.mean(ts[1:])))
+    exp = b.results()[:4]
+    bad = sum(int((o[:calls.nanchors] != e).sum()) for o, e in zip(outs, exp))
+    if bad:
+        raise SystemExit(f"host_chain_kernel drop-in parity FAILED: {bad} mismatching outputs")
+    value = D.sum(float(calls.nanchors)) / t / 1e6
+    return {"value": value, "unit": "Manchors/s", "seconds": t, "vs_kernel_rate": value / kernel_manch,
+            "parity_check": {"anchors": int(calls.nanchors), "bit_exact": True,
+                             "against": "the device batch's score/parent/target/peak"},
+            "note": "std::vector<call_t> in, std::vector<return_t> out (flatten, H2D, chain_dp, D2H, unflatten); "
+                    "the vectors are built outside the clock, as the reference's read_call loop is"}
 
 
 CHAIN_BT_MIN_CNT, CHAIN_BT_MIN_SC = 3, 40  # minimap2 defaults (-n 3, -m 40)
@@ -751,6 +832,27 @@ def bench_bsw(args, D, rank, world, kind="large"):
                 "value": cells_all / t / 1e9, "unit": "GCUPS", "seconds": t,
                 "note": "BandedPairWiseSW::getScores16's C ABI over the rank's SeqPair[] and sequence buffers: "
                         "H2D + kernels + D2H into the SeqPair array"}}
+            lib = dropin_bench_lib()
+            if lib is not None:
+                log("bsw: getScores16 per 512-pair batch from 16 threads (the reference's loop)")
+                got = np.zeros((max(pairs.n, 1), 6), np.int32)
+                par7, mat = params.as_array(), params.mat_array()  # kept alive across the calls
+                ts = []
+                for _ in range(2):
+                    ts.append(lib.bench_bsw_batches(par7.ctypes.data, mat.ctypes.data,
+                                                    pairs.n, sp.ctypes.data, pairs.tgt.ctypes.data,
+                                                    pairs.qry.ctypes.data, 512, 16, got.ctypes.data))
+                t = D.max(float(min(ts)))
+                bad = int((got[:pairs.n] != out6[:pairs.n]).any(axis=1).sum())
+                if bad:
+                    raise SystemExit(f"getScores16 per-batch drop-in parity FAILED: {bad} pairs")
+                v = cells_all / t / 1e9
+                out["dropin_e2e"]["getScores16_per_batch"] = {
+                    "value": v, "unit": "GCUPS", "seconds": t, "vs_kernel_rate": v / gcups,
+                    "parity_check": {"pairs": int(pairs.n), "bit_exact": True, "against": "the device batch's out6"},
+                    "note": "BandedPairWiseSW::getScores16 on 512-pair batches taken dynamically by 16 host "
+                            "threads, one object each, as main_banded.cpp:896-924 (each batch's idr/idq index "
+                            "its own buffers, as loadPairs lays them out)"}
     b.close()
     return out
 
@@ -840,6 +942,9 @@ def bench_phmm(args, D, rank, world, kind="large"):
             log("phmm: drop-in end to end")
             job.close()
             e2e = phmm_dropin_e2e(args, D, ta, cells, rank, world)
+            log("phmm: computelikelihoodsboth once per batch")
+            e2e["computelikelihoodsboth_per_batch"] = phmm_dropin_per_batch(
+                args, D, batches, rank, world, gcups, res if world == 1 else None)
             if world == 1:
                 e2e["bin/phmm"] = phmm_cli_e2e(batches, full.cells())
             out["dropin_e2e"] = e2e
@@ -907,6 +1012,9 @@ def bench_fmi(args, D, rank, world):
         e2e = {"gb_fmi_search": {"value": reads_all / t / 1e6, "unit": "Mreads/s", "seconds": t,
                                  "note": "enc_qdb + lengths H2D, fmi.cpp batch pipeline, all SMEMs + per-batch "
                                          "counts D2H (index already resident)"}}
+        if args.fmi_class_reads > 0:
+            log("fmi: FMI_search class drop-in (fmi.cpp's per-batch loop, 16 threads)")
+            e2e["FMI_search_class"] = fmi_class_e2e(args, D, fmi, ref, idx, codes, lens, mreads)
     sa = bench_sa(args, D, rank, world, fmi, idx, rs, codes, lens)
     rs.close()
     small = None if args.no_small else bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref)
@@ -1043,6 +1151,60 @@ def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full
     return shard_proxy(args, full_ms, full_value, "Mreads/s", t_rank)
 
 
+def fmi_class_e2e(args, D, fmi, ref, idx, codes, lens, kernel_mreads):
+    """The FMI_search class drop-in (lib/libgb_fmi_dropin.so) driven by fmi.cpp:253-348's batch loop
+    (tests/cpp/fmi_class_driver.cpp: per 512-read batch getSMEMsAllPosOneThread, reseeding through
+    getSMEMsOnePosOneThread, bwtSeedStrategyAllPosOneThread, sortSMEMs) from 16 host threads, over the
+    first --fmi-class-reads reads of the rank's shard; the driver's own clock around the batch loop.
+    Its sorted per-batch SMEMs are compared with the batched search's (bit for bit)."""
+    import subprocess
+    import tempfile
+    drv = os.path.join(ROOT, "tests", "_build", "fmi_class_driver")
+    if not os.path.exists(drv):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fmi_util
+    m = min(len(lens), args.fmi_class_reads) // 512 * 512
+    if m == 0:
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        prefix = os.path.join(td, "ref")
+        fmi.Index.build(ref, out_path=prefix + ".bwt.2bit.64").close()
+        rb, ob = os.path.join(td, "reads.bin"), os.path.join(td, "out.bin")
+        with open(rb, "wb") as f:
+            f.write(np.array([m, codes.shape[1]], np.int32).tobytes() + lens[:m].astype(np.int32).tobytes()
+                    + np.ascontiguousarray(codes[:m]).tobytes())
+        r = subprocess.run([drv, prefix, rb, "512", "19", "16", ob], capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            raise SystemExit(f"fmi class driver failed: {r.stderr[-2000:]}")
+        t = float([ln for ln in r.stderr.splitlines() if ln.startswith("SMEM phase:")][0].split()[2])
+        raw = np.fromfile(ob, np.uint8)
+    o = 8
+    nb = int(raw[:8].view(np.int64)[0])
+    parts = []
+    for _ in range(nb):
+        c = raw[o:o + 24].view(np.int64)
+        o += 24
+        k = int(c.sum())
+        parts.append(raw[o:o + 40 * k].view(fmi_util.SMEM_DTYPE))
+        o += 40 * k
+    got = np.concatenate(parts)
+    r2 = fmi.Reads(idx, codes[:m], lens[:m])
+    r2.search(19)
+    sm, tot, _, _ = r2.results(batch_size=512)
+    r2.close()
+    same = len(got) == tot and all((got[f] == sm[f]).all() for f in ("rid", "m", "n", "k", "l", "s"))
+    if not same:
+        raise SystemExit("FMI_search class drop-in parity FAILED against the batched search")
+    t = D.max(t)
+    value = D.sum(float(m)) / t / 1e6
+    return {"value": value, "unit": "Mreads/s", "seconds": t, "reads": int(m), "vs_kernel_rate": value / kernel_mreads,
+            "parity_check": {"reads": int(m), "smems": int(tot), "bit_exact": True,
+                             "against": "the batched search (gb_fmi_search) on the same reads"},
+            "note": "fmi.cpp's batch loop over the FMI_search class methods, 512-read batches from 16 host threads "
+                    "(tests/cpp/fmi_class_driver.cpp), timed around the loop; index loaded before the clock"}
+
+
 def bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref):
     """fmi 'small' (1 M reads, fmi_output:19) over the same index."""
     log("fmi small: timed search")
@@ -1158,6 +1320,8 @@ def main():
                     help="fmi human-scale leg: reference length in Gbp (one GPU only; 0 = off)")
     ap.add_argument("--fmi-human-reads", type=int, default=4_000_000)
     ap.add_argument("--fmi-human-check", type=int, default=20_000, help="human-scale reads checked vs the oracle")
+    ap.add_argument("--fmi-class-reads", type=int, default=2_000_000,
+                    help="reads of the FMI_search class drop-in leg (0 = off)")
     ap.add_argument("--bsw-pairs", type=int, default=10_606_460, help="bsw pairs in the 'large' set")
     ap.add_argument("--only", default=None, help="comma list of legs: phmm,fmi,chain,bsw,fmi_human (default all)")
     ap.add_argument("--no-small", action="store_true", help="skip the 'small'-set legs")
