@@ -19,6 +19,9 @@
 #include <algorithm>
 #include <atomic>
 #include <climits>
+#include <condition_variable>
+#include <mutex>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -716,7 +719,12 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     GB_ARG(false, "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
   }
   std::vector<uint32_t> order((size_t)n);
-  {
+  if (n < (1 << 16)) {
+    // small batches: a stable comparison sort (the counting sort's 1.3 M-entry histogram would cost
+    // more than the call)
+    for (int64_t p = 0; p < n; ++p) order[(size_t)p] = (uint32_t)p;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+  } else {
     std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * kQB * kTB + 1, 0);
     for (int64_t p = 0; p < n; ++p) cnt[keys[p]]++;
     int64_t acc = 0;
@@ -940,9 +948,244 @@ int gb_bsw_batch_timing(gb_bsw_batch *B, float *kernel_ms) {
   return GB_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- small calls (the reference's 512-pair getScores16 batches, main_banded.cpp:896-924) ----------
+// A pair-per-lane launch lasts as long as its slowest pair's whole DP (~0.5 ms), so a call of a few
+// hundred pairs is latency-bound. Small calls instead run every pair on the wave-per-pair kernel
+// (rows are wave-wide scans: a pair takes tens of microseconds), with the call's bytes packed on the
+// host into one pinned staging buffer -- descriptors, the pairs' own target and query bytes (the
+// caller's fixed-stride buffers are mostly padding), zeroed counters -- moved by one H2D copy, and
+// the results back by one D2H copy on the calling thread's stream.
+constexpr int64_t kSmallCall = 16384;  // pairs; GB_BSW_SMALL overrides (0 = never)
+
+struct SmallWs {
+  int device = -1, num_cus = 256;
+  hipStream_t stream = nullptr;
+  uint8_t *h = nullptr, *d = nullptr;
+  size_t hcap = 0, dcap = 0;
+};
+
+int64_t small_call_limit() {
+  const char *e = getenv("GB_BSW_SMALL");  // read per call: tests switch paths inside one process
+  return e ? (int64_t)atoll(e) : kSmallCall;
+}
+
+size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+struct SmallReq {
+  const gb_bsw_params *params;
+  gb_seqpair *pairs;
+  int64_t n;
+  const uint8_t *ref, *qer;
+  int64_t *total_cells;
+  int status = GB_OK;
+  bool done = false;
+};
+
+SmallWs *small_ws(int dev, int *st) {
+  // one workspace per (host thread, device); never freed (see gb_bsw_get_scores16_ex)
+  thread_local std::vector<SmallWs *> wss;
+  for (auto *w : wss)
+    if (w->device == dev) return w;
+  auto *W = new SmallWs();
+  W->device = dev;
+  hipError_t e = hipDeviceGetAttribute(&W->num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&W->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    gb::set_error("getScores16 workspace: %s", hipGetErrorString(e));
+    *st = GB_ERR_HIP;
+    return nullptr;
+  }
+  wss.push_back(W);
+  return W;
+}
+
+// One launch for a group of requests with the same parameters: their pairs are concatenated (and
+// their sequences packed) into W's staging buffer, run on the wave-per-pair kernel, and each
+// request's SeqPair fields and cell total written back.
+int small_group(SmallWs *W, const std::vector<SmallReq *> &g) {
+  const gb_bsw_params *params = g[0]->params;
+  int mx = 0;
+  for (int k = 0; k < 25; ++k) mx = std::max(mx, (int)params->mat[k]);
+  int64_t n = 0, tb = 0, qb = 0;
+  for (const SmallReq *r : g) {
+    n += r->n;
+    for (int64_t p = 0; p < r->n; ++p) {
+      tb += r->pairs[p].len1;
+      qb += r->pairs[p].len2;
+    }
+  }
+  // staging / device layout: [Pair n | list n | ctl 16 B | tgt | qry] (uploaded) [out6 n | cells n]
+  const size_t o_list = up16(sizeof(gbbsw::Pair) * (size_t)n), o_ctl = o_list + up16(4 * (size_t)n),
+               o_tgt = o_ctl + 16, o_qry = o_tgt + up16((size_t)tb), up_bytes = o_qry + up16((size_t)qb),
+               o_out = up_bytes, o_cells = o_out + up16(24 * (size_t)n), d_bytes = o_cells + up16(4 * (size_t)n);
+  if (std::max(up_bytes, d_bytes - o_out) > W->hcap) {
+    if (W->h) (void)hipHostFree(W->h);
+    W->h = nullptr;
+    W->hcap = 0;
+    const size_t want = std::max<size_t>(2 * std::max(up_bytes, d_bytes - o_out), 1 << 20);
+    GB_HIP(hipHostMalloc(&W->h, want, hipHostMallocDefault));
+    W->hcap = want;
+  }
+  if (d_bytes > W->dcap) {
+    (void)hipFree(W->d);
+    W->d = nullptr;
+    W->dcap = 0;
+    const size_t want = std::max<size_t>(2 * d_bytes, 1 << 20);
+    GB_HIP(hipMalloc(&W->d, want));
+    W->dcap = want;
+  }
+  uint8_t *h = W->h;
+  auto *P = reinterpret_cast<gbbsw::Pair *>(h);
+  auto *list = reinterpret_cast<uint32_t *>(h + o_list);
+  int64_t to = 0, qo = 0, k = 0;
+  for (const SmallReq *r : g)
+    for (int64_t p = 0; p < r->n; ++p, ++k) {
+      const gb_seqpair &sp = r->pairs[p];
+      std::memcpy(h + o_tgt + to, r->ref + sp.idr, (size_t)sp.len1);
+      std::memcpy(h + o_qry + qo, r->qer + sp.idq, (size_t)sp.len2);
+      P[k] = gbbsw::Pair{to, qo, sp.len1, sp.len2, sp.h0, gbbsw::adjust_w(params->w, sp.len2, mx, *params)};
+      list[k] = (uint32_t)k;
+      to += sp.len1;
+      qo += sp.len2;
+    }
+  std::memset(h + o_ctl, 0, 16);
+  GB_HIP(hipMemcpyAsync(W->d, h, up_bytes, hipMemcpyHostToDevice, W->stream));
+  gbbsw::Args A;
+  A.pairs = reinterpret_cast<const gbbsw::Pair *>(W->d);
+  A.list = reinterpret_cast<const uint32_t *>(W->d + o_list);
+  A.n = n;
+  A.tgt = W->d + o_tgt;
+  A.qry = W->d + o_qry;
+  A.out6 = reinterpret_cast<int32_t *>(W->d + o_out);
+  A.cells = reinterpret_cast<int32_t *>(W->d + o_cells);
+  A.total_cells = reinterpret_cast<unsigned long long *>(W->d + o_ctl);
+  A.next = reinterpret_cast<unsigned int *>(W->d + o_ctl + 8);
+  A.o_del = params->o_del;
+  A.e_del = params->e_del;
+  A.o_ins = params->o_ins;
+  A.e_ins = params->e_ins;
+  A.zdrop = params->zdrop;
+  std::memset(A.mat, 0, sizeof(A.mat));
+  std::memcpy(A.mat, params->mat, 25);
+  const int64_t blocks = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)W->num_cus * gbbsw::kBlocksPerCU, (n + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
+  hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0, W->stream, A);
+  GB_HIP(hipGetLastError());
+  // out6 and the per-pair cell counts back in one copy (they are adjacent on the device)
+  GB_HIP(hipMemcpyAsync(h, W->d + o_out, d_bytes - o_out, hipMemcpyDeviceToHost, W->stream));
+  GB_HIP(hipStreamSynchronize(W->stream));
+  const auto *r6 = reinterpret_cast<const int32_t *>(h);
+  const auto *cells = reinterpret_cast<const int32_t *>(h + (o_cells - o_out));
+  k = 0;
+  for (SmallReq *r : g) {
+    int64_t c = 0;
+    for (int64_t p = 0; p < r->n; ++p, ++k) {
+      const int32_t *o = r6 + 6 * k;
+      gb_seqpair &sp = r->pairs[p];
+      sp.score = o[0];
+      sp.qle = o[1];
+      sp.tle = o[2];
+      sp.gtle = o[3];
+      sp.gscore = o[4];
+      sp.max_off = o[5];
+      c += cells[k];
+    }
+    if (r->total_cells) *r->total_cells = c;
+  }
+  return GB_OK;
+}
+
+// Flat combining across host threads: the reference calls getScores16 on 512-pair batches from an
+// OpenMP team, each call synchronous. A calling thread queues its request; whichever thread finds
+// fewer than kLeaders groups in flight takes every queued request with the same parameters and runs
+// them as one launch, the others wait for their request to be marked done. While one group runs, the
+// next one accumulates, so groups grow to about one call per waiting thread.
+constexpr int kLeaders = 2;  // groups in flight per device (one packing/copying while one computes)
+
+struct Combiner {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<SmallReq *> pending;
+  int leaders = 0;
+};
+
+Combiner &combiner(int dev) {
+  static std::mutex gm;
+  static std::vector<std::pair<int, Combiner *>> all;
+  std::lock_guard<std::mutex> lk(gm);
+  for (auto &c : all)
+    if (c.first == dev) return *c.second;
+  all.emplace_back(dev, new Combiner());  // never freed, like the workspaces
+  return *all.back().second;
+}
+
+int small_call(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref, int64_t ref_bytes,
+               const uint8_t *qer, int64_t qer_bytes, int64_t *total_cells) {
+  for (int64_t p = 0; p < n; ++p) {
+    const gb_seqpair &sp = pairs[p];
+    GB_ARG(sp.len2 >= 1 && sp.len2 <= GB_BSW_MAX_QLEN && sp.len1 >= 0,
+           "gb_bsw_get_scores16: pair %lld has len1=%d len2=%d (need len2 in [1,%d])", (long long)p, sp.len1,
+           sp.len2, GB_BSW_MAX_QLEN);
+    GB_ARG(sp.idr >= 0 && sp.idr + sp.len1 <= ref_bytes && sp.idq >= 0 && sp.idq + sp.len2 <= qer_bytes,
+           "gb_bsw_get_scores16: pair %lld lies outside the sequence buffers", (long long)p);
+  }
+  int dev = 0;
+  GB_HIP(hipGetDevice(&dev));
+  int st = GB_OK;
+  SmallWs *W = small_ws(dev, &st);
+  if (!W) return st;
+  SmallReq me{params, pairs, n, ref, qer, total_cells};
+  Combiner &C = combiner(dev);
+  std::unique_lock<std::mutex> lk(C.m);
+  C.pending.push_back(&me);
+  while (!me.done) {
+    if (C.leaders < kLeaders && !C.pending.empty()) {
+      // lead: take the queued requests with the first one's parameters (up to kSmallCall pairs)
+      std::vector<SmallReq *> g, rest;
+      int64_t np = 0;
+      for (SmallReq *r : C.pending)
+        if ((g.empty() || (!std::memcmp(r->params, g[0]->params, sizeof(gb_bsw_params)) && np + r->n <= kSmallCall)))
+          g.push_back(r), np += r->n;
+        else
+          rest.push_back(r);
+      C.pending.swap(rest);
+      C.leaders++;
+      lk.unlock();
+      const int gst = small_group(W, g);
+      std::string err = gst ? gb_last_error() : std::string();
+      lk.lock();
+      for (SmallReq *r : g) {
+        r->status = gst;
+        r->done = true;
+      }
+      C.leaders--;
+      C.cv.notify_all();
+      if (gst && !me.done) gb::set_error("%s", err.c_str());
+    } else {
+      C.cv.wait(lk);
+    }
+  }
+  lk.unlock();
+  if (me.status && me.status != GB_OK) gb::set_error("gb_bsw_get_scores16: a combined getScores16 launch failed");
+  return me.status;
+}
+
+}  // namespace
+
+extern "C" {
+
 int gb_bsw_get_scores16_ex(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const uint8_t *ref,
                            int64_t ref_bytes, const uint8_t *qer, int64_t qer_bytes, int64_t *total_cells) {
   gb::Range range_("gb.bsw.get_scores16");
+  GB_ARG(params && n >= 0 && (n == 0 || pairs), "gb_bsw_get_scores16: bad arguments");
+  GB_ARG(params->e_del > 0 && params->e_ins > 0, "gb_bsw_get_scores16: gap extension must be > 0");
+  GB_ARG(ref_bytes >= 0 && qer_bytes >= 0 && (ref_bytes == 0 || ref) && (qer_bytes == 0 || qer),
+         "gb_bsw_get_scores16: bad sequence buffers");
+  if (n > 0 && n <= small_call_limit()) return small_call(params, pairs, n, ref, ref_bytes, qer, qer_bytes, total_cells);
   // one cached batch per (host thread, device): the reference calls getScores16 once per batch of
   // 512 pairs (main_banded.cpp:896-909), so streams, events and buffers are reused across calls.
   // Never freed (freeing at thread exit could run after the HIP runtime is torn down).

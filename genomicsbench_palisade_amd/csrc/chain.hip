@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -699,9 +700,20 @@ int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, con
     if ((st = batch_new(&B))) return st;
     ws.emplace_back(dev, B);
   }
+  const bool hp = getenv("GB_CHAIN_HOSTPROF") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   if ((st = batch_fill(B, ncalls, offsets, avg_qspan, params4, x, y))) return st;
+  const auto t1 = std::chrono::steady_clock::now();
   st = gb_chain_batch_run(B);
+  if (!st && hp) st = gb_chain_batch_sync(B);
+  const auto t2 = std::chrono::steady_clock::now();
   if (!st) st = gb_chain_batch_results(B, scores, parents, targets, peak_scores, nullptr);
+  if (hp) {
+    const auto t3 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[gb_chain] fill (validate, H2D, plan) %.2f ms, run %.2f ms, results %.2f ms\n", ms(t0, t1),
+            ms(t1, t2), ms(t2, t3));
+  }
   return st;
 }
 

@@ -41,4 +41,16 @@ int gb_set_device(int device) {
   GB_HIP(hipSetDevice(device));
   return GB_OK;
 }
+
+int gb_host_alloc(void **ptr, size_t bytes) {
+  GB_ARG(ptr, "gb_host_alloc: null ptr");
+  *ptr = nullptr;
+  GB_HIP(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  return GB_OK;
+}
+
+int gb_host_free(void *ptr) {
+  if (ptr) GB_HIP(hipHostFree(ptr));
+  return GB_OK;
+}
 }

@@ -6,6 +6,8 @@
 #ifndef GB_H
 #define GB_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -24,6 +26,10 @@ int gb_device_count(int *count);
 /* Select the HIP device for subsequent gb_* calls on this thread (objects stay bound to the
  * device that was current when they were created). */
 int gb_set_device(int device);
+/* Page-locked host memory (hipHostMalloc), for the C++ drop-ins' staging buffers: copies from it to
+ * the device run at DMA rate instead of through the runtime's pageable bounce buffers. */
+int gb_host_alloc(void **ptr, size_t bytes);
+int gb_host_free(void *ptr);
 
 #ifdef __cplusplus
 }

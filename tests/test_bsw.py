@@ -247,3 +247,51 @@ def test_gpu_cli_scores8(tmp_path):
     gen.write_bsw_file(fin, bad)
     r = subprocess.run([exe, "-pairs", str(fin), "-bits", "8"], capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "8-bit" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("limit", ["0", "100000000"])
+def test_gpu_get_scores16_small_and_batch_paths(golden, monkeypatch, limit):
+    """getScores16's two paths -- the pair-per-lane batch launch (GB_BSW_SMALL=0) and the small-call
+    path (packed pinned staging + the wave-per-pair kernel for every pair, used below GB_BSW_SMALL
+    pairs) -- both reproduce ksw_extend2 on the golden sets (six parameter sets) and on long queries
+    and targets."""
+    from genomicsbench_palisade_amd import GbError, set_device
+    set_device(0)
+    monkeypatch.setenv("GB_BSW_SMALL", limit)
+    p, sets = golden
+    for name, (P, exp) in sets.items():
+        sp = bsw.get_scores16(p, P)
+        assert_same(np.stack([sp[f] for f in FIELDS], axis=1), exp, f"{name} (limit {limit})")
+    q = gen.bsw_pairs(3000, seed=17, qlen=(120, 255), extra=(0, 900))
+    P = bsw.default_params()
+    sp = bsw.get_scores16(q, P)
+    assert_same(np.stack([sp[f] for f in FIELDS], axis=1), oracle_lib.bsw_oracle(q, P, nthreads=8)[0], "long")
+    bad = gen.BswPairs(np.zeros(4, np.uint8), np.array([2], np.int64), np.array([4], np.int32), np.zeros(4, np.uint8),
+                       np.zeros(1, np.int64), np.array([4], np.int32), np.array([10], np.int32))
+    with pytest.raises(GbError):
+        bsw.get_scores16(bad, P)
+
+
+@pytest.mark.gpu
+def test_gpu_dropin_512_pair_batches_from_threads():
+    """BandedPairWiseSW::getScores16 called per 512-pair batch from 8 host threads (one object each), each
+    batch's idr/idq indexing its own buffers, as main_banded.cpp:896-924 calls it
+    (tests/cpp/dropin_bench.cpp): every pair equals ksw_extend2."""
+    import ctypes
+    from conftest import ROOT
+    from genomicsbench_palisade_amd import set_device
+    set_device(0)
+    lib = ctypes.CDLL(os.path.join(ROOT, "tests", "_build", "libdropin_bench.so"))
+    vp = ctypes.c_void_p
+    lib.bench_bsw_batches.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.bench_bsw_batches.restype = ctypes.c_double
+    p = gen.bsw_pairs(20000, seed=23)
+    P = bsw.default_params()
+    sp = bsw.seqpairs(p)
+    par7, mat = P.as_array(), P.mat_array()
+    got = np.zeros((p.n, 6), np.int32)
+    t = lib.bench_bsw_batches(par7.ctypes.data, mat.ctypes.data, p.n, sp.ctypes.data, p.tgt.ctypes.data,
+                              p.qry.ctypes.data, 512, 8, got.ctypes.data)
+    assert t > 0
+    assert_same(got, oracle_lib.bsw_oracle(p, P, nthreads=8)[0], "512-pair batches")
