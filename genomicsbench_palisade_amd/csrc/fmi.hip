@@ -30,6 +30,7 @@
 #include "../../include/gb.h"
 #include "gb_common.h"
 #include "fmi_index.h"
+#include "fmi_wave.h"
 
 namespace gbfmi {
 
@@ -164,7 +165,7 @@ constexpr int kQBases = 160;
 constexpr int kQW = kQBases / 8 + 1;  // words per lane row; odd, so same-word reads are conflict-free
 static_assert(kQBases % 32 == 0, "staging copies 32 bases per 16-byte load");
 
-template <bool kLdsQ>
+template <bool kLdsQ, bool kNT>
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
   const DevIndex F = A.F;
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     // ---- one backwardExt per lane per trip --------------------------------------------------
     int64_t ko, lo, so;
     const unsigned long long tB = prof ? clock64() : 0;
-    bwt_ext(F, rk, rl, rs, rb, ko, lo, so);
+    bwt_ext<kNT>(F, rk, rl, rs, rb, ko, lo, so);
     calls_read++;
     unsigned long long tC = 0;
     if (prof) {
@@ -640,17 +641,11 @@ struct HeavyArgs {
   int64_t *trace;  // GB_FMI_FLAGS & 8 (as SearchArgs::trace), or null
 };
 
-__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
-  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(v >> 32), src);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
 __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
   __shared__ PEnt La[kHeavyMaxLen + 1], Lb[kHeavyMaxLen + 1];
   __shared__ uint8_t Q[kHeavyMaxLen];
   const DevIndex F = A.F;
   const int lane = threadIdx.x;
-  const uint64_t below = (1ull << lane) - 1;
   const int nh = *(volatile const int32_t *)A.heavy_n;
   for (int t = blockIdx.x; t < nh; t += gridDim.x) {
     const int rd = A.heavy[t];
@@ -696,98 +691,9 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
       nout++;
     };
 
-    // getSMEMsOnePosOneThread for one position (FMI_search.cpp:1015-1176); returns next_x
+    uint32_t *const calls_p = &calls;
     auto one_pos = [&](int x, int min_intv) -> int {
-      int next_x = x + 1;
-      int a = Q[x];
-      if (a >= 4) return next_x;
-      int64_t ck = count_of(F, a), cl = count_of(F, 3 - a), cs = count_of(F, a + 1) - ck;
-      const uint32_t cm = (uint32_t)x;
-      int numPrev = 0, j;
-      for (j = x + 1; j < L; j++) {  // forward extension, wave-uniform
-        next_x = j + 1;
-        a = Q[j];
-        if (a >= 4) break;
-        int64_t ko, lo, so;
-        bwt_ext(F, cl, ck, cs, 3 - a, ko, lo, so);
-        calls++;
-        if (so != cs) {
-          if (lane == 0) La[numPrev] = pack_ent(Ent{ck, cl, cs, cm, (uint32_t)(j - 1)});
-          numPrev++;
-        }
-        if (so < min_intv) {
-          next_x = j;
-          break;
-        }
-        ck = lo;
-        cl = ko;
-        cs = so;
-      }
-      if (cs >= min_intv) {
-        if (lane == 0) La[numPrev] = pack_ent(Ent{ck, cl, cs, cm, (uint32_t)(j - 1)});
-        numPrev++;
-      }
-      __syncthreads();
-      // backward search: list r[p] = La[numPrev - 1 - p] at first (the reversed prev array), then
-      // each step's pushes in order
-      PEnt *in = La, *out = Lb;
-      bool rev = true;
-      for (j = x - 1; j >= 0; j--) {
-        a = Q[j];
-        if (a > 3) break;
-        int numCurr = 0;
-        bool found = false;
-        int64_t carry_s = -1;
-        for (int c0 = 0; c0 < numPrev; c0 += 64) {
-          const int p = c0 + lane;
-          const bool valid = p < numPrev;
-          PEnt pe{};
-          Ent e{};
-          int64_t ko = 0, lo = 0, so = 0;
-          if (valid) {
-            pe = in[rev ? numPrev - 1 - p : p];
-            e = unpack_ent(pe);
-            bwt_ext(F, e.k, e.l, e.s, a, ko, lo, so);
-          }
-          const bool v = valid && so >= min_intv;
-          const bool em = valid && so < min_intv && (e.n - e.m + 1) >= (uint32_t)A.min_seed_len;
-          const uint64_t vm = __ballot(v);
-          if (!found) {
-            const uint64_t bm = __ballot(v || em);
-            if (bm == 0) continue;  // the first loop has not stopped yet: nothing pushed
-            found = true;
-            const int f = __builtin_ctzll(bm);
-            if (!((vm >> f) & 1)) {  // the first loop stops on an emit (lanes before f have neither)
-              PEnt fe;
-              fe.w0 = (uint64_t)shfl64((int64_t)pe.w0, f);
-              fe.w1 = (uint64_t)shfl64((int64_t)pe.w1, f);
-              const Ent ee = unpack_ent(fe);
-              emit(ee.k, ee.l, ee.s, ee.m, ee.n);
-            }
-          }
-          const uint64_t lowv = vm & below;
-          const int64_t sp = shfl64(so, lowv ? 63 - __builtin_clzll(lowv) : lane);
-          const bool push = v && so != (lowv ? sp : carry_s);
-          const uint64_t pm = __ballot(push);
-          if (push) out[numCurr + __popcll(pm & below)] = pack_ent(Ent{ko, lo, so, (uint32_t)j, e.n});
-          numCurr += __popcll(pm);
-          if (vm) carry_s = shfl64(so, 63 - __builtin_clzll(vm));
-        }
-        calls += numPrev;
-        __syncthreads();
-        PEnt *tmp = in;
-        in = out;
-        out = tmp;
-        rev = false;
-        numPrev = numCurr;
-        if (numCurr == 0) break;
-      }
-      if (numPrev != 0) {
-        const Ent e = unpack_ent(in[rev ? numPrev - 1 : 0]);
-        if ((e.n - e.m + 1) >= (uint32_t)A.min_seed_len) emit(e.k, e.l, e.s, e.m, e.n);
-      }
-      __syncthreads();
-      return next_x;
+      return wave_one_pos(F, Q, L, x, min_intv, A.min_seed_len, La, Lb, lane, *calls_p, emit);
     };
 
     // getSMEMsAllPosOneThread (min_intv 1)
@@ -810,35 +716,7 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
     }
     const int n2 = nout - n1;
     // bwtSeedStrategyAllPosOneThread (FMI_search.cpp:1243-1326), max_intv 20
-    for (int x = 0; x < L;) {
-      int next_x = x + 1;
-      int a = Q[x];
-      if (a >= 4) {
-        x = next_x;
-        continue;
-      }
-      int64_t ck = count_of(F, a), cl = count_of(F, 3 - a), cs = count_of(F, a + 1) - ck;
-      const uint32_t cm = (uint32_t)x;
-      bool done = false;
-      for (int j = x + 1; j < L; j++) {
-        next_x = j + 1;
-        a = Q[j];
-        if (a >= 4) break;
-        int64_t ko, lo, so;
-        bwt_ext(F, cl, ck, cs, 3 - a, ko, lo, so);
-        calls++;
-        ck = lo;
-        cl = ko;
-        cs = so;
-        if (cs < 20 && (uint32_t)(j - (int)cm + 1) >= (uint32_t)(A.min_seed_len + 1)) {
-          if (cs > 0) emit(ck, cl, cs, cm, (uint32_t)j);
-          x = j + 1;
-          done = true;
-          break;
-        }
-      }
-      if (!done) x = next_x;
-    }
+    wave_last_seeds(F, Q, L, 20, A.min_seed_len + 1, calls, emit);  // fmi.cpp passes minSeedLen + 1
     if (lane == 0) {
       A.counts[rd] = nout;
       A.phase[3 * rd + 0] = n1;
@@ -1367,10 +1245,20 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
-    if (R->stride <= gbfmi::kQBases)
-      hipLaunchKernelGGL(gbfmi::smem_search<true>, dim3(blocks), dim3(64), 0, R->stream, A);
-    else
-      hipLaunchKernelGGL(gbfmi::smem_search<false>, dim3(blocks), dim3(64), 0, R->stream, A);
+    // GB_FMI_NT=1: the Occ32 gathers as non-temporal loads (load_occ32)
+    const char *nte = getenv("GB_FMI_NT");
+    const bool nt = nte && *nte == '1';
+    if (R->stride <= gbfmi::kQBases) {
+      if (nt)
+        hipLaunchKernelGGL((gbfmi::smem_search<true, true>), dim3(blocks), dim3(64), 0, R->stream, A);
+      else
+        hipLaunchKernelGGL((gbfmi::smem_search<true, false>), dim3(blocks), dim3(64), 0, R->stream, A);
+    } else {
+      if (nt)
+        hipLaunchKernelGGL((gbfmi::smem_search<false, true>), dim3(blocks), dim3(64), 0, R->stream, A);
+      else
+        hipLaunchKernelGGL((gbfmi::smem_search<false, false>), dim3(blocks), dim3(64), 0, R->stream, A);
+    }
     GB_HIP(hipGetLastError());
     if (A.budget != INT32_MAX) {
       gbfmi::HeavyArgs H;

@@ -24,6 +24,7 @@
 #include "../../include/gb.h"
 #include "../../include/gb_fmi.h"
 #include "fmi_index.h"
+#include "fmi_wave.h"
 #include "gb_common.h"
 
 namespace gbfmi {
@@ -225,6 +226,57 @@ __global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
   if ((threadIdx.x & 63) == 0 && calls) atomicAdd(A.calls, (unsigned long long)calls);
 }
 
+// The same tasks, one wave per task (fmi_wave.h): a call of a few hundred tasks is latency-bound --
+// one lane per task lasts as long as its longest task's chain of dependent gathers, where a wave runs
+// each backward step's extensions in parallel. Records and their order per task are those of
+// fmi_task_kernel. Reads up to kWaveMaxLen bases (the `prev` lists live in LDS).
+constexpr int kWaveMaxLen = 256;
+
+template <int kMode>
+__global__ __launch_bounds__(64) void fmi_task_wave(TaskArgs A) {
+  __shared__ PEnt La[kWaveMaxLen + 1], Lb[kWaveMaxLen + 1];
+  __shared__ uint8_t Q[kWaveMaxLen];
+  const int lane = threadIdx.x;
+  for (int t = blockIdx.x; t < A.ntasks; t += gridDim.x) {
+    const uint32_t rid = (uint32_t)A.rid[t];
+    const int L = A.lens[rid];
+    const uint8_t *q = A.qdb + A.offs[rid];
+    for (int i = lane; i < L; i += 64) Q[i] = q[i];
+    __syncthreads();
+    int cnt = 0;
+    uint32_t calls = 0, round = 0;
+    auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
+      if (lane == 0 && cnt < A.cap) {
+        TSmem o;
+        o.rid = rid;
+        o.m = m;
+        o.n = n;
+        o.round = round;
+        o.k = k;
+        o.l = l;
+        o.s = s;
+        A.out[(size_t)t * A.cap + cnt] = o;
+      }
+      cnt++;
+    };
+    if (kMode == kOnePos) {
+      const int nx = wave_one_pos(A.F, Q, L, A.qpos[t], A.intv[t], A.min_seed_len, La, Lb, lane, calls, emit);
+      if (lane == 0) A.next_pos[t] = (int16_t)nx;
+    } else if (kMode == kAllPos) {
+      for (int x = 0; x < L; round++)  // the do-while of FMI_search.cpp:1203-1236 as seen by this read
+        x = (int16_t)wave_one_pos(A.F, Q, L, x, A.intv[t], A.min_seed_len, La, Lb, lane, calls, emit);
+      if (lane == 0) A.rounds[t] = (int32_t)round;
+    } else {
+      wave_last_seeds(A.F, Q, L, A.intv[t], A.min_seed_len, calls, emit);
+    }
+    if (lane == 0) {
+      A.counts[t] = cnt;
+      if (calls) atomicAdd(A.calls, (unsigned long long)calls);
+    }
+    __syncthreads();
+  }
+}
+
 // Per host thread and device: stream and grow-only device buffers (the reference's methods are
 // called from OpenMP threads sharing one FMI_search object).
 struct Workspace {
@@ -363,13 +415,25 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     GB_HIP(hipMemcpyAsync(W.buf[3], rid.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     GB_HIP(hipMemcpyAsync(W.buf[4], qpos.data(), sizeof(int16_t) * n, hipMemcpyHostToDevice, s));
     GB_HIP(hipMemcpyAsync(W.buf[5], intv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    const dim3 grid((unsigned)((n + 63) / 64)), block(64);
-    if (mode == kOnePos)
-      hipLaunchKernelGGL(fmi_task_kernel<kOnePos>, grid, block, 0, s, A);
-    else if (mode == kAllPos)
-      hipLaunchKernelGGL(fmi_task_kernel<kAllPos>, grid, block, 0, s, A);
-    else
-      hipLaunchKernelGGL(fmi_task_kernel<kLast>, grid, block, 0, s, A);
+    // a wave per task when the reads fit its LDS lists (GB_FMI_TASK_WAVE=0: a lane per task)
+    const char *we = getenv("GB_FMI_TASK_WAVE");
+    if (maxlen <= kWaveMaxLen && !(we && *we == '0')) {
+      const dim3 grid((unsigned)std::min<int64_t>(n, 65535)), block(64);
+      if (mode == kOnePos)
+        hipLaunchKernelGGL(fmi_task_wave<kOnePos>, grid, block, 0, s, A);
+      else if (mode == kAllPos)
+        hipLaunchKernelGGL(fmi_task_wave<kAllPos>, grid, block, 0, s, A);
+      else
+        hipLaunchKernelGGL(fmi_task_wave<kLast>, grid, block, 0, s, A);
+    } else {
+      const dim3 grid((unsigned)((n + 63) / 64)), block(64);
+      if (mode == kOnePos)
+        hipLaunchKernelGGL(fmi_task_kernel<kOnePos>, grid, block, 0, s, A);
+      else if (mode == kAllPos)
+        hipLaunchKernelGGL(fmi_task_kernel<kAllPos>, grid, block, 0, s, A);
+      else
+        hipLaunchKernelGGL(fmi_task_kernel<kLast>, grid, block, 0, s, A);
+    }
     GB_HIP(hipGetLastError());
     std::vector<int32_t> ctl(2 * (size_t)n);
     std::vector<int16_t> np(n);

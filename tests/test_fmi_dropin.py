@@ -120,12 +120,15 @@ def _oracle_phases(oi, codes, lens, bc, maxlen, min_seed_len):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("size,nreads,L,batch,threads,seed,build,tile",
-                         [(300_000, 1500, 151, 512, 3, 3, False, ""), (120_000, 700, 101, 64, 2, 4, True, ""),
-                          (200_000, 1100, 151, 512, 2, 5, False, "100")])
-def test_class_driver_matches_oracle(tmp_path, size, nreads, L, batch, threads, seed, build, tile):
+@pytest.mark.parametrize("size,nreads,L,batch,threads,seed,build,tile,wave",
+                         [(300_000, 1500, 151, 512, 3, 3, False, "", ""), (120_000, 700, 101, 64, 2, 4, True, "", ""),
+                          (200_000, 1100, 151, 512, 2, 5, False, "100", ""),
+                          (300_000, 1500, 151, 512, 3, 3, False, "", "0"), (150_000, 600, 300, 128, 2, 6, False, "", "")])
+def test_class_driver_matches_oracle(tmp_path, size, nreads, L, batch, threads, seed, build, tile, wave):
     """tile: GB_FMI_TASK_TILE, tasks per launch of the per-call kernels (the scratch bound; 100 forces
-    several tiles per call, with the overflow pass inside each)."""
+    several tiles per call, with the overflow pass inside each). wave: GB_FMI_TASK_WAVE -- reads up to
+    256 bases run a wave per task (fmi_wave.h), "0" forces a lane per task; 300-base reads always take
+    the lane kernel."""
     ref = gen.fmi_reference(size, seed=seed, repeat_frac=0.15)
     codes, lens = gen.fmi_reads(ref, nreads, read_len=L, seed=seed + 50, sub_rate=0.02, n_rate=0.003)
     lens = lens.copy()
@@ -146,7 +149,11 @@ def test_class_driver_matches_oracle(tmp_path, size, nreads, L, batch, threads, 
         f.write(np.array([nreads, L], np.int32).tobytes() + lens.astype(np.int32).tobytes() + codes.tobytes())
     out = tmp_path / "out.bin"
     args = [DRIVER, prefix, str(rb), str(batch), "19", str(threads), str(out)] + (["build"] if build else [])
-    env = dict(os.environ, GB_FMI_TASK_TILE=tile) if tile else None
+    env = dict(os.environ)
+    if tile:
+        env["GB_FMI_TASK_TILE"] = tile
+    if wave:
+        env["GB_FMI_TASK_WAVE"] = wave
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     if build:
