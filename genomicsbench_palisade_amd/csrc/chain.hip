@@ -480,12 +480,16 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
     GB_HIP(hipMemcpy(B->d_aq, avg_qspan, (size_t)ncalls * sizeof(float), hipMemcpyHostToDevice));
     GB_HIP(hipMemcpy(B->d_par4, params4, (size_t)ncalls * 16, hipMemcpyHostToDevice));
   }
+  // the anchors go up on the batch stream while the host plans the block table (from page-locked
+  // caller memory -- the host_chain_kernel drop-in stages there -- the copy runs beside the plan)
   if (na) {
-    GB_HIP(hipMemcpy(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice));
-    GB_HIP(hipMemcpy(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice));
+    GB_HIP(hipMemcpyAsync(B->d_x, x, (size_t)na * 8, hipMemcpyHostToDevice, B->stream));
+    GB_HIP(hipMemcpyAsync(B->d_y, y, (size_t)na * 8, hipMemcpyHostToDevice, B->stream));
   }
   // the block table: whole calls, or long calls as speculative segments (chain_split.hip)
-  return gbchain::split_plan(B, offsets, x, params4);
+  const int st = gbchain::split_plan(B, offsets, x, params4);
+  GB_HIP(hipStreamSynchronize(B->stream));  // the caller may free x / y on return
+  return st;
 }
 
 }  // namespace

@@ -123,6 +123,7 @@ struct SearchArgs {
                          // wave-cooperative pass (smem_heavy); INT32_MAX = never
   int32_t *heavy;        // reads handed over (capacity nreads) and their count
   int32_t *heavy_n;
+  int32_t prefetch;      // claim the next read when taking one (GB_FMI_PREFETCH, default off)
   int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof,
                          // 8 = per-read trace (start / end wall clock, backwardExt calls) into `trace`
   int64_t *trace;
@@ -165,7 +166,7 @@ constexpr int kQBases = 160;
 constexpr int kQW = kQBases / 8 + 1;  // words per lane row; odd, so same-word reads are conflict-free
 static_assert(kQBases % 32 == 0, "staging copies 32 bases per 16-byte load");
 
-template <bool kLdsQ, bool kNT>
+template <bool kLdsQ>
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
   const DevIndex F = A.F;
@@ -264,7 +265,9 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             st = DONE;
             break;
           }
-          nslot = atomicAdd(A.next_read, 1);
+          // prefetch: claim the following read now so its atomic's latency hides behind this read;
+          // but a claimed read waits behind the current one, which lengthens the grid's tail
+          if (A.prefetch) nslot = atomicAdd(A.next_read, 1);
           rd = A.list ? A.list[slot] : slot;
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     // ---- one backwardExt per lane per trip --------------------------------------------------
     int64_t ko, lo, so;
     const unsigned long long tB = prof ? clock64() : 0;
-    bwt_ext<kNT>(F, rk, rl, rs, rb, ko, lo, so);
+    bwt_ext(F, rk, rl, rs, rb, ko, lo, so);
     calls_read++;
     unsigned long long tC = 0;
     if (prof) {
@@ -1220,6 +1223,8 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     const char *h = getenv("GB_FMI_HEAVY");
     const int budget = h ? atoi(h) : gbfmi::kHeavyBudget;
     A.budget = (budget > 0 && R->stride <= gbfmi::kHeavyMaxLen) ? budget : INT32_MAX;
+    const char *pf = getenv("GB_FMI_PREFETCH");
+    A.prefetch = pf && *pf == '1';
   }
   A.heavy = R->d_heavy;
   A.heavy_n = R->d_ctl + 4;
@@ -1245,20 +1250,10 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
-    // GB_FMI_NT=1: the Occ32 gathers as non-temporal loads (load_occ32)
-    const char *nte = getenv("GB_FMI_NT");
-    const bool nt = nte && *nte == '1';
-    if (R->stride <= gbfmi::kQBases) {
-      if (nt)
-        hipLaunchKernelGGL((gbfmi::smem_search<true, true>), dim3(blocks), dim3(64), 0, R->stream, A);
-      else
-        hipLaunchKernelGGL((gbfmi::smem_search<true, false>), dim3(blocks), dim3(64), 0, R->stream, A);
-    } else {
-      if (nt)
-        hipLaunchKernelGGL((gbfmi::smem_search<false, true>), dim3(blocks), dim3(64), 0, R->stream, A);
-      else
-        hipLaunchKernelGGL((gbfmi::smem_search<false, false>), dim3(blocks), dim3(64), 0, R->stream, A);
-    }
+    if (R->stride <= gbfmi::kQBases)
+      hipLaunchKernelGGL(gbfmi::smem_search<true>, dim3(blocks), dim3(64), 0, R->stream, A);
+    else
+      hipLaunchKernelGGL(gbfmi::smem_search<false>, dim3(blocks), dim3(64), 0, R->stream, A);
     GB_HIP(hipGetLastError());
     if (A.budget != INT32_MAX) {
       gbfmi::HeavyArgs H;

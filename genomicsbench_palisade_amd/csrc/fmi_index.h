@@ -105,39 +105,20 @@ __device__ __forceinline__ int64_t count_of(const DevIndex &F, int a) {
   return a == 0 ? F.count[0] : a == 1 ? F.count[1] : a == 2 ? F.count[2] : a == 3 ? F.count[3] : F.count[4];
 }
 
-// One Occ32 block. NT: a non-temporal (streaming) load -- the block is inserted into L2 as the
-// first to evict, so the random gathers (little reuse below the first extension steps) do not push
-// out the search's `prev` lists, whose hot set is what the L2 can keep.
-typedef unsigned int gb_u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ Occ32 load_occ32(const Occ32 *p) {
-  if constexpr (NT) {
-    const gb_u32x4 *q = reinterpret_cast<const gb_u32x4 *>(p);
-    const gb_u32x4 a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
-    Occ32 L;
-    L.bwt[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
-    L.bwt[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
-    L.cnt[0] = (uint64_t)b.x | ((uint64_t)b.y << 32);
-    L.cnt[1] = (uint64_t)b.z | ((uint64_t)b.w << 32);
-    return L;
-  } else {
-    return *p;
-  }
-}
-
 // backwardExt(smem{k,l,s}, a) -> {k', l', s'} (FMI_search.cpp:1536-1565). One 32-byte block covers
 // 64 rows; when sp and ep share a block the second load is skipped.
-template <bool NT = false>
 __device__ __forceinline__ void bwt_ext(const DevIndex &F, int64_t k, int64_t l, int64_t s, int a,
                                         int64_t &ko, int64_t &lo, int64_t &so) {
   const int64_t sp = k, ep = k + s;
   const int64_t bs = sp >> 6, be = ep >> 6;
   // the second line only when sp and ep fall in different lines (a duplicate request for the same
   // line measured 10 % slower overall than the occasional wait for A)
-  const Occ32 A = load_occ32<NT>(F.occ + bs);
+  // (non-temporal loads, so the gathers would not evict the `prev` lists from L2, measured slower:
+  // 130 -> 183 ms for 4 M reads, and FETCH / WRITE_SIZE up, 319 -> 338 / 69 -> 93 GB, r03g)
+  const Occ32 A = F.occ[bs];
   Occ32 B;
   if (be != bs)
-    B = load_occ32<NT>(F.occ + be);
+    B = F.occ[be];
   else
     B = A;
   int64_t os[4], oe[4];

@@ -10,3 +10,5 @@ for NT in 0 1; do
   GB_FMI_NT=$NT FMI_PROBE_READS=4000000 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/ntw_r03g_$NT -o run -- python3 tools/fmi_probe.py > /dev/null 2>&1 || exit 1
 done
 echo pmc done
+timeout -k 10 200 python -u tools/phmm_dropin_probe.py 2>&1 | grep -v amdgpu.ids
+for PF in 1 0; do GB_FMI_PREFETCH=$PF FMI_TAIL_TAG=r03g_pf$PF timeout -k 10 240 python -u tools/fmi_tail_probe.py 2>&1 | grep -v amdgpu.ids | sed "s/^/PF=$PF /"; done
