@@ -868,9 +868,9 @@ def bench_phmm(args, D, rank, world, kind="large"):
     batches = gen.phmm_dataset(kind, nb, seed=set_seed(args, 1, rank))
     full = TestcaseArray.from_batches(batches)
     if args.scaling == "strong":
-        ta, (lo, hi) = shard.shard_testcases(full, rank, world)
+        ta, tidx = shard.shard_testcases(full, rank, world)
     else:
-        ta, (lo, hi) = full, (0, full.n)
+        ta, tidx = full, np.arange(full.n)
     job = phmm.DeviceBatch(ta)
     ntc, cells, _ = job.stats()
     # one checked pass first (its results give the f64 share), then the warm-up steps run straight into
@@ -907,7 +907,8 @@ def bench_phmm(args, D, rank, world, kind="large"):
     out = {
         "value": gcups, "unit": "GCUPS", "elapsed": elapsed, "ntc": full.n, "cells": full.cells(), "cells_all_ranks": cells_all,
         "f64_frac": float(used.mean()) if ta.n else 0.0,
-        "shard": shard_note(args, "testcases", lo, hi, full.n, world),
+        "shard": (f"{len(tidx)} of {full.n} testcases: the rank-{rank} 1/{world} piece of every batch (stratified)"
+                  if args.scaling == "strong" and world > 1 else shard_note(args, "testcases", 0, full.n, full.n, world)),
         "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
     }

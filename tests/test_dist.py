@@ -1,7 +1,7 @@
 """Multi-process (N>1) path on CPU: world_size-2 gloo process groups exercise bench.py's Dist
 (barrier, max-over-ranks time, sum-over-ranks work), its timed_steps bracket and set_seed, and the
 strong-scaling shard -> compute -> concatenate flow bench.py uses for all four legs (shard.py:
-testcases by cells, whole 512-read batches, calls by anchors, pairs by cell estimate), with the C
+testcases as a cell-balanced piece of every batch, whole 512-read batches, calls by anchors, pairs by cell estimate), with the C
 oracles standing in for the per-GPU kernels (CPU-only container): the two ranks' outputs
 concatenate to the 1-rank output exactly."""
 import json
@@ -38,7 +38,7 @@ pairs = gen.bsw_pairs(500, seed=bench.set_seed(args, 4, rank))
 psub, _ = shard.shard_pairs(pairs, rank, world)
 out = oracle_lib.bsw_oracle(psub, bsw.default_params(), 1)[0]
 ta = TestcaseArray.from_batches(gen.phmm_dataset("small", 3, seed=bench.set_seed(args, 1, rank)))
-tsub, trange = shard.shard_testcases(ta, rank, world)
+tsub, tidx = shard.shard_testcases(ta, rank, world)
 pr = np.zeros(tsub.n); rf = np.zeros(tsub.n, np.float32); rd = np.zeros(tsub.n)
 import ctypes
 if tsub.n:
@@ -51,7 +51,7 @@ fs, fbc, _ = oi.run(codes[rlo:rhi], lens[rlo:rhi], batch_size=512)
 fs["rid"] += rlo
 import torch.distributed as dist
 got = [None] * world
-dist.all_gather_object(got, {"chain": sc.tolist(), "bsw": out.tolist(), "phmm": pr.tolist(), "trange": list(trange),
+dist.all_gather_object(got, {"chain": sc.tolist(), "bsw": out.tolist(), "phmm": pr.tolist(), "tidx": [int(x) for x in tidx],
                              "fmi": [list(map(int, t)) for t in zip(fs["rid"], fs["m"], fs["n"], fs["k"], fs["l"], fs["s"])],
                              "fmi_bc": fbc.tolist(), "rrange": [rlo, rhi],
                              "max": mx, "sum": sm, "range": [lo, hi], "timed_steps_ms": ms})
@@ -120,8 +120,12 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
     pr, rf, rd = np.zeros(ta.n), np.zeros(ta.n, np.float32), np.zeros(ta.n)
     oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(ta.arr), ta.n, pr.ctypes.data, rf.ctypes.data,
                                           rd.ctypes.data, None, 1)
-    assert got[0]["trange"][1] == got[1]["trange"][0] and got[1]["trange"][1] == ta.n
-    assert (np.array(got[0]["phmm"] + got[1]["phmm"]).view(np.uint64) == pr.view(np.uint64)).all()
+    # phmm: the ranks' stratified pieces (1/2 of every batch) partition the job and gather back
+    idx = np.array(got[0]["tidx"] + got[1]["tidx"])
+    assert (np.sort(idx) == np.arange(ta.n)).all()
+    gathered = np.zeros(ta.n)
+    gathered[idx] = np.array(got[0]["phmm"] + got[1]["phmm"])
+    assert (gathered.view(np.uint64) == pr.view(np.uint64)).all()
     # fmi: whole 512-read batches per rank; SMEM lists and per-batch counts concatenate
     import fmi_util
     ref = gen.fmi_reference(60_000, seed=5)
