@@ -1,0 +1,6 @@
+# r03j: the driver's round-end sequence (all GPU tests, smoke, the default bench line)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/pytest_r03j.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_r03j.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 1100 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_r03j.json 2> gpurun_out/bench_r03j.err; echo bench rc=$?
