@@ -162,17 +162,31 @@ __device__ void heap_sort(gb_smem *a, int n) {
 // Reads up to kQBases bases are staged, 4 bits per base, in the lane's LDS row when the lane takes
 // the read (one pass of dword loads from the nibble-packed copy d_q4), so the base lookups of the
 // state machine are LDS reads instead of dependent global byte loads. Longer reads read d_qdb.
-constexpr int kQBases = 160;
-constexpr int kQW = kQBases / 8 + 1;  // words per lane row; odd, so same-word reads are conflict-free
-static_assert(kQBases % 32 == 0, "staging copies 32 bases per 16-byte load");
+// 152 bases (the reference's 151-bp reads): 19 words per lane row, odd, so same-word reads are
+// conflict-free, and with the 8 KB `prev` list head (kTop) a wave's LDS is 13 056 B -- 12 waves per
+// CU in 512-B allocation granules (160 bases' 21-word rows made it 13 568 B: 11 waves)
+constexpr int kQBases = 152;
+constexpr int kQW = kQBases / 8;
+static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
 
-template <bool kLdsQ>
+// kTop: the first entries of every `prev` list (list indices p < kTop, where the backward loop's
+// reads and its in-place compaction concentrate as the lists shrink) live in LDS, the rest in the
+// wave-interleaved scratch. List index p of a list whose forward phase pushed n entries is push
+// k = n - 1 - p, kept in LDS slot k & (kTop - 1) = (c - p) & (kTop - 1) with c = n - 1: during the
+// forward phase the slots hold the last kTop pushes (a push evicts the one kTop before it to its
+// scratch position), and the compaction writes r'[q] into r[q]'s slot, already read. 8 KB per wave
+// beside the 5.25 KB of staged read codes: 12 waves per CU still fit.
+template <bool kLdsQ, int kTop>  // kTop 0: every entry in the scratch
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
+  constexpr bool kTopLds = kTop > 0;
   __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
+  __shared__ PEnt Ltop[kTopLds ? kTop * 64 : 1];
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
   PList prev;
   prev.base = A.scratch + (size_t)(gid >> 6) * A.stride * 64 + (gid & 63);
+  PEnt *const top = Ltop + (kTopLds ? threadIdx.x : 0);
+  int tc = 0;  // c of the current list (kTopLds)
   uint32_t calls = 0, calls_read = 0;  // backwardExt calls (all reads / this read)
 
   int st = NEXT_READ;
@@ -199,6 +213,35 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   // compacted in place behind the read position, so a prefetched entry is never overwritten
   // before it is used.)
   PEnt head{};
+  // forward push of e (push index k = numPrev): scratch position L - 1 - k, or with kTopLds the LDS
+  // ring of the last kTop pushes
+  auto push_fwd = [&](const Ent &e) {
+    const PEnt pe = pack_ent(e);
+    if constexpr (kTopLds) {
+      const int k = numPrev;
+      PEnt *slot = top + (size_t)(k & (kTop - 1)) * 64;
+      if (k >= kTop) prev.base[(size_t)(L - 1 - (k - kTop)) * 64] = *slot;
+      *slot = pe;
+    } else {
+      prev.base[(size_t)(L - 1 - numPrev) * 64] = pe;
+    }
+    numPrev++;
+    head = pe;
+  };
+  // list index p of the current reversed list (p >= 1; r[0] is `head`)
+  auto get_r = [&](int p_) -> PEnt {
+    if constexpr (kTopLds)
+      if (p_ < kTop) return top[(size_t)((tc - p_) & (kTop - 1)) * 64];
+    return prev.base[(size_t)(r0 + p_) * 64];
+  };
+  auto put_r = [&](int q_, const PEnt &pe) {
+    if constexpr (kTopLds)
+      if (q_ < kTop) {
+        top[(size_t)((tc - q_) & (kTop - 1)) * 64] = pe;
+        return;
+      }
+    prev.base[(size_t)(r0 + q_) * 64] = pe;
+  };
 
   int cap = A.cap;  // slots of the current output area (kCap, or kBigCap once promoted)
   int kb_cur = -1;  // the big slot of the current read, if promoted
@@ -277,10 +320,11 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             const int n4 = (L + 31) >> 5;
             for (int w = 0; w < n4; w++) {
               const uint4 v = src[w];
-              qrow[4 * w] = v.x;
-              qrow[4 * w + 1] = v.y;
-              qrow[4 * w + 2] = v.z;
-              qrow[4 * w + 3] = v.w;
+              // the row holds kQW words: the last 16-byte chunk's words past it are beyond the read
+              if (4 * w < kQW) qrow[4 * w] = v.x;
+              if (4 * w + 1 < kQW) qrow[4 * w + 1] = v.y;
+              if (4 * w + 2 < kQW) qrow[4 * w + 2] = v.z;
+              if (4 * w + 3 < kQW) qrow[4 * w + 3] = v.w;
             }
           }
           o = A.slots + (size_t)slot * A.cap;
@@ -340,11 +384,10 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           if (cs >= min_intv) {
             Ent e;
             e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);  // current n = j-1
-            prev.put(L - 1 - numPrev, e);
-            numPrev++;
-            head = pack_ent(e);
+            push_fwd(e);
           }
           r0 = L - numPrev;
+          tc = numPrev - 1;
           j = x - 1;
           st = BWD_ITER;
           break;
@@ -375,7 +418,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
             }
             break;
           }
-          cur = p == 0 ? head : prev.base[(size_t)(r0 + p) * 64];
+          cur = p == 0 ? head : get_r(p);
           {
             const Ent ce = unpack_ent(cur);
             rk = ce.k;
@@ -505,9 +548,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       if (ns != cs) {  // push the current SMEM (prevArray[numPrev] = smem; numPrev += s_neq)
         Ent e;
         e.k = ck; e.l = cl; e.s = cs; e.m = cm; e.n = (uint32_t)(j - 1);
-        prev.put(L - 1 - numPrev, e);
-        numPrev++;
-        head = pack_ent(e);
+        push_fwd(e);
       }
       if (ns < min_intv) {
         next_x = j;
@@ -540,20 +581,22 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           curr_s = (int)so;
           Ent ne;
           ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
-          if (numCurr == 0) head = pack_ent(ne);  // r[0] of the next j
-          prev.put(r0 + numCurr++, ne);
+          const PEnt pne = pack_ent(ne);
+          if (numCurr == 0) head = pne;  // r[0] of the next j
+          put_r(numCurr++, pne);
           first = false;
         }
       } else if (so >= min_intv && so != (int64_t)curr_s) {
         curr_s = (int)so;
         Ent ne;
         ne.k = ko; ne.l = lo; ne.s = so; ne.m = (uint32_t)j; ne.n = e.n;
-        if (numCurr == 0) head = pack_ent(ne);
-        prev.put(r0 + numCurr++, ne);
+        const PEnt pne = pack_ent(ne);
+        if (numCurr == 0) head = pne;
+        put_r(numCurr++, pne);
       }
       p++;
       if (p < numPrev) {  // BWD_P's request for the next list entry, inline
-        cur = prev.base[(size_t)(r0 + p) * 64];
+        cur = get_r(p);
         const Ent ce = unpack_ent(cur);
         rk = ce.k;
         rl = ce.l;
@@ -1250,10 +1293,26 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
-    if (R->stride <= gbfmi::kQBases)
-      hipLaunchKernelGGL(gbfmi::smem_search<true>, dim3(blocks), dim3(64), 0, R->stream, A);
-    else
-      hipLaunchKernelGGL(gbfmi::smem_search<false>, dim3(blocks), dim3(64), 0, R->stream, A);
+    // GB_FMI_TOP: entries of the `prev` list head kept in LDS, 8 (default), 4 or 0
+    const char *te = getenv("GB_FMI_TOP");
+    const int top = te ? atoi(te) : 8;
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, R->stream, A); };
+    const char *qe = getenv("GB_FMI_QLDS");  // 0: read codes from global memory, not staged in LDS
+    if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0')) {
+      if (top >= 8)
+        launch(gbfmi::smem_search<true, 8>);
+      else if (top >= 4)
+        launch(gbfmi::smem_search<true, 4>);
+      else
+        launch(gbfmi::smem_search<true, 0>);
+    } else {
+      if (top >= 8)
+        launch(gbfmi::smem_search<false, 8>);
+      else if (top >= 4)
+        launch(gbfmi::smem_search<false, 4>);
+      else
+        launch(gbfmi::smem_search<false, 0>);
+    }
     GB_HIP(hipGetLastError());
     if (A.budget != INT32_MAX) {
       gbfmi::HeavyArgs H;

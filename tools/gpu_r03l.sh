@@ -1,0 +1,12 @@
+# r03l: fmi list head in LDS at 4 / 8 entries, 19-word read rows (12 waves per CU): parity + timing
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fmi_gpu.py tests/test_fmi_large.py tests/test_fmi_dropin.py -m gpu > gpurun_out/pytest_r03l.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_r03l.log; [ $rc -eq 0 ] || exit 1
+for T in 8 4 0; do
+  GB_FMI_TOP=$T FMI_PROBE_READS=4000000 timeout -k 10 120 python -u tools/fmi_probe.py 2>&1 | grep -v amdgpu.ids | sed "s/^/TOP=$T /" || exit 1
+done
+for T in 8 4; do
+  GB_FMI_TOP=$T FMI_PROBE_READS=4000000 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/topw_r03l_$T -o run -- python3 tools/fmi_probe.py > /dev/null 2>&1 || exit 1
+done
+FMI_TAIL_TAG=r03l timeout -k 10 240 python -u tools/fmi_tail_probe.py 2>&1 | grep -v amdgpu.ids | grep -v "^ "
+echo done
