@@ -885,9 +885,11 @@ int lanes_for_device() {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
-  // 12 resident waves per CU (3 per SIMD): large set 29.99 vs 29.74 Mreads/s at 16, 'small' (1 M
-  // reads, ~5 per lane) 18.47 vs 17.62 -- fewer lanes, shorter per-wave tails (tools/fmi_small_occ.sh)
-  const int waves = e ? std::max(1, atoi(e)) : 12;
+  // 11 resident waves per CU: the most the LDS holds with the staged read codes and the 8-entry
+  // `prev` list head (13 056 B per wave in 2 KB allocation granules). Round 2 chose 12 (3 per SIMD)
+  // over 16 (tools/fmi_small_occ.sh); the read codes from global memory instead (GB_FMI_QLDS=0)
+  // allow 16 but ran slower: 4 M reads 115 ms at 16 waves vs 111 ms staged at 11 (r03m).
+  const int waves = e ? std::max(1, atoi(e)) : 11;
   return cus * waves * 64;
 }
 
