@@ -129,11 +129,12 @@ __device__ int wave_one_pos(const DevIndex &F, const uint8_t *Q, int L, int x, i
 }
 
 // bwtSeedStrategyAllPosOneThread for one read (FMI_search.cpp:1256-1323), wave-uniform;
-// min_seed_len as the caller passes it (fmi.cpp passes minSeedLen + 1).
+// min_seed_len as the caller passes it (fmi.cpp passes minSeedLen + 1). x0: the position to start
+// from (the loop carries nothing else from one x to the next, so a read handed over at x resumes there).
 template <class Emit>
 __device__ void wave_last_seeds(const DevIndex &F, const uint8_t *Q, int L, int max_intv, int min_seed_len,
-                                uint32_t &calls, Emit &&emit) {
-  for (int x = 0; x < L;) {
+                                uint32_t &calls, Emit &&emit, int x0 = 0) {
+  for (int x = x0; x < L;) {
     int next_x = x + 1;
     int a = Q[x];
     if (a >= 4) {
