@@ -16,9 +16,14 @@ full = TestcaseArray.from_batches(gen.phmm_dataset("large", int(os.environ.get("
 of, r = int(os.environ.get("PHMM_OF", "8")), int(os.environ.get("PHMM_RANK", "0"))
 for name, ta in [("full", full), (f"shard {r}/{of}", shard.shard_testcases(full, r, of)[0])]:
     for rows in os.environ.get("PHMM_ROWS", "default").split(";"):
-        if rows == "default":
-            os.environ.pop("GB_PHMM_STACK_ROWS", None)
-        else:
+        # a setting: "default", a GB_PHMM_STACK_ROWS value, or env assignments "K=V,K=V"
+        for k in ("GB_PHMM_STACK_ROWS", "GB_PHMM_F64_ROWS"):
+            os.environ.pop(k, None)
+        if "=" in rows:
+            for kv in rows.split(","):
+                k, v = kv.split("=")
+                os.environ[k] = v
+        elif rows != "default":
             os.environ["GB_PHMM_STACK_ROWS"] = rows
         job = phmm.DeviceBatch(ta)
         for _ in range(3):
@@ -33,5 +38,5 @@ for name, ta in [("full", full), (f"shard {r}/{of}", shard.shard_testcases(full,
         a, b, c = job.timing()
         ntc, cells, nf64 = job.stats()
         job.close()
-        print(f"{name:12s} rows {rows:8s}: {ntc} testcases, {cells / 1e9:.2f} G cells, f64 {nf64}; wall {wall:.3f} ms "
+        print(f"{name:12s} {rows:24s}: {ntc} testcases, {cells / 1e9:.2f} G cells, f64 {nf64}; wall {wall:.3f} ms "
               f"({cells / wall / 1e6:.1f} GCUPS); f32 {a:.3f} ms, f64 {b:.3f} ms, step {c:.3f} ms", flush=True)
