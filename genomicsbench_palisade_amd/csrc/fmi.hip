@@ -102,68 +102,23 @@ enum State : int {
 
 // ---- reads handed over --------------------------------------------------------------------------
 // A lane gives a read up when its forward phase leaves a long `prev` list (list_t: a repeat, whose
-// backward search the lane would extend one entry per trip), when it has run kHeavyBudget
-// backwardExt calls (a heavy read: a few per thousand make 2.5-25x the median's calls), or -- off by
-// default -- in the grid's tail (drain_k / drain_calls). A heavy read's backwardExt calls cost a
-// lane ~5 us each under load and the wave-per-read routine ~0.19 us. The read resumes, one wave per read
-// (heavy_read), from the last position boundary its lane passed, recorded in an HRec: phase `mode`
-// (1 all positions, 2 reseeding, 3 LAST) at `pos` (x, or the reseeding index), with nout SMEMs
-// already in its slot (n1 / n2 as far as known), `calls` backwardExt calls made up to there, and
-// kb >= 0 when they are in that big slot. Waves whose lanes are all done take the records while the
-// kernel still runs; smem_heavy after it takes whatever is left (nothing, unless help is off).
+// backward search the lane would extend one entry per trip) or when it has run kHeavyBudget
+// backwardExt calls (a heavy read: a few per thousand make 2.5-25x the median's calls); such a read's
+// calls cost a lane ~5 us each under load and the wave-per-read routine (heavy_read, smem_heavy after
+// the search) ~0.19 us. The read resumes there from the last position boundary its lane passed,
+// recorded in an HRec: phase `mode` (1 all positions, 2 reseeding, 3 LAST) at `pos` (x, or the
+// reseeding index), with nout SMEMs already in its slot (n1 / n2 as far as known), `calls`
+// backwardExt calls made up to there, and kb >= 0 when they are in that big slot.
+// Measured and dropped in round 3 (r03o-r03v): the search's own waves taking the records once their
+// lanes were done (inlined, the routine slowed the lane loop ~3 %; every XCD has its own L2 and they
+// are not coherent inside a kernel, so the records had to stay on the XCD that wrote them), and
+// handing over ordinary reads in the grid's tail (their forward extensions run one gather at a time
+// in the wave routine too, and the per-trip ballot slowed the search 8 %).
 constexpr int kHeavyMaxLen = 256;   // reads up to this long can be handed over (lists in LDS)
 constexpr int kHeavyBudget = 2000;  // backwardExt calls before a lane hands its read over
 struct HRec {
-  int32_t rd, tag, mp, nout, n1, n2, calls, kb;  // mp = mode << 16 | pos
+  int32_t rd, mp, nout, n1, n2, calls, kb, pad;  // mp = mode << 16 | pos
 };
-// The records queue per XCD: a read is resumed on the XCD whose lane gave it up, so its record and
-// the SMEMs already in its slot are in the L2 the resuming wave reads through (every XCD has its own
-// L2, and they are not kept coherent with each other inside a kernel; agent-scope loads and stores
-// below only bypass the CU's L1). A full queue just means the lane keeps its read.
-constexpr int kXcds = 8;
-__device__ __forceinline__ int xcc_id() {
-  int x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & (kXcds - 1);
-}
-
-// What another CU of the XCD reads during the same kernel -- a handed-over read's SMEMs and its
-// record -- is stored and read with agent-scope accesses, which do not stop in the CU's L1.
-__device__ __forceinline__ void st_ag(int32_t *p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_ag(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t ld_ag(const int32_t *p) {
-  return __hip_atomic_load(const_cast<int32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_ag(const uint64_t *p) {
-  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-static_assert(sizeof(gb_smem) == 40 && offsetof(gb_smem, k) == 16, "gb_smem: five 8-byte words");
-__device__ __forceinline__ void put_smem(gb_smem *p, uint32_t rid, uint32_t m, uint32_t n, int64_t k, int64_t l,
-                                         int64_t s) {
-  uint64_t *w = reinterpret_cast<uint64_t *>(p);
-  st_ag(w, (uint64_t)rid | ((uint64_t)m << 32));
-  st_ag(w + 1, (uint64_t)n);
-  st_ag(w + 2, (uint64_t)k);
-  st_ag(w + 3, (uint64_t)l);
-  st_ag(w + 4, (uint64_t)s);
-}
-__device__ __forceinline__ void put_smem(gb_smem *p, const gb_smem &e) { put_smem(p, e.rid, e.m, e.n, e.k, e.l, e.s); }
-__device__ __forceinline__ gb_smem get_smem(const gb_smem *p) {
-  const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
-  const uint64_t w0 = ld_ag(w), w1 = ld_ag(w + 1);
-  gb_smem e;
-  e.rid = (uint32_t)w0;
-  e.m = (uint32_t)(w0 >> 32);
-  e.n = (uint32_t)w1;
-  e.k = (int64_t)ld_ag(w + 2);
-  e.l = (int64_t)ld_ag(w + 3);
-  e.s = (int64_t)ld_ag(w + 4);
-  return e;
-}
 
 struct SearchArgs {
   DevIndex F;
@@ -187,18 +142,11 @@ struct SearchArgs {
   unsigned long long *bwt_calls;
   int32_t budget;        // a read still running after this many backwardExt calls is handed over to
                          // the wave-per-read routine (heavy_read); INT32_MAX = never
-  HRec *recs;            // reads handed over: kXcds queues of xcap records, with per-queue counters
-  int32_t *hq;           // hq[16 x] = records published on XCD x, hq[16 x + 1] = taken
-  int32_t xcap;
-  int32_t drain_k;       // once the read queue is drained, a wave with <= drain_k lanes still
-                         // running hands their reads over too (0 = never)
-  int32_t drain_calls;   // ... and so does a lane whose read has made >= drain_calls calls (0 = never)
+  HRec *recs;            // reads handed over (capacity nreads: a read is handed over at most once)
+  int32_t *nrecs;        // and their count
   int32_t list_t;        // a read whose forward phase leaves a `prev` list of >= list_t entries (a
                          // repeat: the backward search will extend them one by one) is handed over
                          // at once (0 = never)
-  int32_t help;          // waves whose lanes are all done take handed-over reads (0: smem_heavy after
-                         // the kernel does them all)
-  int32_t epoch;         // this search's record tag
   int32_t prefetch;      // claim the next read when taking one (GB_FMI_PREFETCH, default off)
   int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof,
                          // 8 = per-read trace (start / end wall clock, backwardExt calls) into `trace`
@@ -233,7 +181,7 @@ __device__ void heavy_read(const Args &A, const HRec &r, PEnt *La, PEnt *Lb, uin
       if (kb < kMaxOvf) {
         gb_smem *big = A.big + (size_t)kb * kBigCap;
         if (lane == 0) {
-          for (int i = 0; i < kCap; i++) put_smem(big + i, get_smem(o + i));
+          for (int i = 0; i < kCap; i++) big[i] = o[i];
           A.ovf_list[kb] = rd;
         }
         o = big;
@@ -241,7 +189,16 @@ __device__ void heavy_read(const Args &A, const HRec &r, PEnt *La, PEnt *Lb, uin
       }
     }
     if (nout < cap) {
-      if (lane == 0) put_smem(o + nout, (uint32_t)rd, m, n, k, l, s);
+      if (lane == 0) {
+        gb_smem e;
+        e.rid = (uint32_t)rd;
+        e.m = m;
+        e.n = n;
+        e.k = k;
+        e.l = l;
+        e.s = s;
+        o[nout] = e;
+      }
     } else {
       ovf = true;
     }
@@ -260,7 +217,7 @@ __device__ void heavy_read(const Args &A, const HRec &r, PEnt *La, PEnt *Lb, uin
     for (int ridx = mode0 == 2 ? pos0 : 0; ridx < n1 && ridx < cap; ridx++) {
       int mm = 0, nn = 0, ss = 0;
       if (lane == 0) {
-        const gb_smem e = get_smem(o + ridx);  // possibly stored by the lane that gave the read up
+        const gb_smem e = o[ridx];  // (the first n of them stored by the lane that gave the read up)
         mm = (int)e.m;
         nn = (int)e.n;
         ss = (int)min<int64_t>(e.s, 1 << 30);
@@ -342,16 +299,8 @@ static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
 template <bool kLdsQ, int kTop>  // kTop 0: every entry in the scratch
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   constexpr bool kTopLds = kTop > 0;
-  // one LDS block: the staged read codes and the list heads while the lanes run reads, then the
-  // lists of heavy_read once they are all done
-  constexpr int kQBytes = kLdsQ ? 64 * kQW * 4 : 16;
-  constexpr int kTopBytes = kTopLds ? kTop * 64 * (int)sizeof(PEnt) : 16;
-  constexpr int kHelpBytes = 2 * (kHeavyMaxLen + 1) * (int)sizeof(PEnt) + kHeavyMaxLen;
-  constexpr int kRaw = kQBytes + kTopBytes > kHelpBytes ? kQBytes + kTopBytes : kHelpBytes;
-  static_assert(kQBytes % 16 == 0, "16-byte aligned list heads");
-  __shared__ uint4 lds_raw[(kRaw + 15) / 16];
-  uint32_t *const Qs = reinterpret_cast<uint32_t *>(lds_raw);
-  PEnt *const Ltop = reinterpret_cast<PEnt *>(reinterpret_cast<char *>(lds_raw) + kQBytes);
+  __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
+  __shared__ PEnt Ltop[kTopLds ? kTop * 64 : 1];
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
   PList prev;
@@ -422,23 +371,30 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       const int kb = atomicAdd(A.ovf_n, 1);
       if (kb < kMaxOvf) {
         gb_smem *big = A.big + (size_t)kb * kBigCap;
-        for (int t = 0; t < kCap; t++) put_smem(big + t, o[t]);  // its own stores: plain loads see them
+        for (int t = 0; t < kCap; t++) big[t] = o[t];
         o = big;
         cap = kBigCap;
         kb_cur = kb;
         A.ovf_list[kb] = rd;
       }
     }
-    if (nout < cap)
-      put_smem(o + nout, (uint32_t)rd, m, n, k, l, s);
-    else
+    if (nout < cap) {
+      gb_smem e;
+      e.rid = (uint32_t)rd;
+      e.m = m;
+      e.n = n;
+      e.k = k;
+      e.l = l;
+      e.s = s;
+      o[nout] = e;
+    } else {
       ovf = true;
+    }
     nout++;
   };
   // the last position boundary this lane passed (see HRec): where a handed-over read resumes
   int b_mode = 1, b_pos = 0, b_nout = 0;
   uint32_t b_calls = 0;
-  bool keep_ok = true;  // false: this read found its XCD's queue full
   bool long_list = false;  // list_t reached (see SearchArgs::list_t)
 
   const bool prof = A.flags & 4;
@@ -451,37 +407,25 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   bool pend = false;
   while (true) {
     const unsigned long long tA = prof ? clock64() : 0;
-    // hand the read over (see HRec): a heavy read, or -- lanes that left the loop found the queue
-    // empty -- one of the last few reads of a wave in the grid's tail
-    bool give = calls_read >= (uint32_t)A.budget || long_list;
-    if (A.drain_k > 0 || A.drain_calls > 0) {
-      const int act = __popcll(__ballot(1));  // lanes still in the loop; < 64: the queue is drained
-      give |= act <= A.drain_k || (act < 64 && A.drain_calls > 0 && calls_read >= (uint32_t)A.drain_calls);
-    }
-    if (give && keep_ok && st != NEXT_READ && st != DONE && st != FINISH) {
-      // what it did after the boundary is dropped (those calls are not counted); a big slot it took
-      // after the boundary is released
-      const int xq = xcc_id();
-      const int k = atomicAdd(A.hq + 16 * xq, 1);
-      if (k < A.xcap) {
-        const int kb = kb_cur >= 0 && b_nout > kCap ? kb_cur : -1;
-        HRec *hr = A.recs + (size_t)xq * A.xcap + k;
-        st_ag(&hr->rd, rd);
-        st_ag(&hr->mp, (b_mode << 16) | b_pos);
-        st_ag(&hr->nout, b_nout);
-        st_ag(&hr->n1, n1);
-        st_ag(&hr->n2, n2);
-        st_ag(&hr->calls, (int32_t)b_calls);
-        st_ag(&hr->kb, kb);
-        if (A.flags & 8) A.trace[3 * (size_t)rd] = t_read;
-        __builtin_amdgcn_s_waitcnt(0);  // the record (and the SMEMs before it) complete, then the tag
-        st_ag(&hr->tag, A.epoch);  // (the calls up to the boundary are counted with the resumed read's)
-        if (kb_cur >= 0 && kb < 0) A.ovf_list[kb_cur] = -1;
-        pend = false;
-        st = NEXT_READ;
-      } else {
-        keep_ok = false;  // the XCD's queue is full: keep the read (and stop asking for this one)
-      }
+    // hand the read over (see HRec): a long list or a heavy read
+    if ((calls_read >= (uint32_t)A.budget || long_list) && st != NEXT_READ && st != DONE && st != FINISH) {
+      // what it did after the boundary is dropped (those calls are not counted; the resumed read
+      // counts the ones up to it); a big slot it took after the boundary is released
+      const int kb = kb_cur >= 0 && b_nout > kCap ? kb_cur : -1;
+      if (kb_cur >= 0 && kb < 0) A.ovf_list[kb_cur] = -1;
+      HRec hr;
+      hr.rd = rd;
+      hr.mp = (b_mode << 16) | b_pos;
+      hr.nout = b_nout;
+      hr.n1 = n1;
+      hr.n2 = n2;
+      hr.calls = (int32_t)b_calls;
+      hr.kb = kb;
+      hr.pad = 0;
+      A.recs[atomicAdd(A.nrecs, 1)] = hr;
+      if (A.flags & 8) A.trace[3 * (size_t)rd] = t_read;
+      pend = false;
+      st = NEXT_READ;
     }
     // ---- advance this lane's state machine to its next backwardExt request --------------------
     bool req = pend;
@@ -524,7 +468,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           nout = 0;
           ovf = false;
           calls_read = 0;
-          keep_ok = true;
           long_list = false;
           mode = 1;
           x = 0;
@@ -848,54 +791,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     }
   }
   atomicAdd(A.bwt_calls, (unsigned long long)calls);
-  if (A.help) {
-    // every lane is done and the read queue is drained: take handed-over reads of this XCD's queue,
-    // one at a time, until none is left. A record published later is taken by the wave that
-    // published it (it comes here after its lanes are done), so every record is taken.
-    __syncthreads();  // the LDS block changes roles
-    PEnt *const La = reinterpret_cast<PEnt *>(lds_raw), *const Lb = La + (kHeavyMaxLen + 1);
-    uint8_t *const Qh = reinterpret_cast<uint8_t *>(Lb + (kHeavyMaxLen + 1));
-    const int lane = threadIdx.x;
-    const int xq = xcc_id();
-    int32_t *const cnt = A.hq + 16 * xq, *const tkn = cnt + 1;
-    const HRec *const q = A.recs + (size_t)xq * A.xcap;
-    while (true) {
-      int t = -1;
-      HRec r{};
-      if (lane == 0) {
-        while (true) {  // the counters by atomics (device-coherent), the claim by compare-and-swap
-          const int n = min(atomicAdd(cnt, 0), A.xcap), tk = atomicAdd(tkn, 0);
-          if (tk >= n) break;
-          if (atomicCAS(tkn, tk, tk + 1) == tk) {
-            t = tk;
-            break;
-          }
-        }
-        if (t >= 0) {
-          const HRec *hr = q + t;
-          while (ld_ag(&hr->tag) != A.epoch) __builtin_amdgcn_s_sleep(2);  // published after the count
-          r.rd = ld_ag(&hr->rd);
-          r.mp = ld_ag(&hr->mp);
-          r.nout = ld_ag(&hr->nout);
-          r.n1 = ld_ag(&hr->n1);
-          r.n2 = ld_ag(&hr->n2);
-          r.calls = ld_ag(&hr->calls);
-          r.kb = ld_ag(&hr->kb);
-        }
-      }
-      // lane 0's values, as scalars (the routine's control flow is then uniform to the compiler)
-      t = __builtin_amdgcn_readfirstlane(t);
-      if (t < 0) break;
-      r.rd = __builtin_amdgcn_readfirstlane(r.rd);
-      r.mp = __builtin_amdgcn_readfirstlane(r.mp);
-      r.nout = __builtin_amdgcn_readfirstlane(r.nout);
-      r.n1 = __builtin_amdgcn_readfirstlane(r.n1);
-      r.n2 = __builtin_amdgcn_readfirstlane(r.n2);
-      r.calls = __builtin_amdgcn_readfirstlane(r.calls);
-      r.kb = __builtin_amdgcn_readfirstlane(r.kb);
-      heavy_read(A, r, La, Lb, Qh, lane);
-    }
-  }
   if (prof && (threadIdx.x & 63) == 0) {
     atomicAdd(&g_fmi_prof[0], p_sm);
     atomicAdd(&g_fmi_prof[1], p_mem);
@@ -917,8 +812,7 @@ struct HeavyArgs {
   const int32_t *lens;
   int32_t stride, min_seed_len, split_len;
   const HRec *recs;  // as SearchArgs
-  const int32_t *hq;
-  int32_t xcap;
+  const int32_t *nrecs;
   gb_smem *slots;  // kCap per read
   gb_smem *big;
   int32_t *counts, *phase, *ovf_list, *ovf_n, *fatal;
@@ -929,18 +823,8 @@ struct HeavyArgs {
 __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
   __shared__ PEnt La[kHeavyMaxLen + 1], Lb[kHeavyMaxLen + 1];
   __shared__ uint8_t Q[kHeavyMaxLen];
-  // the queues' untaken records as one index space (after the kernel: plain loads see them)
-  int beg[kXcds], cum = 0;
-  for (int x = 0; x < kXcds; x++) {
-    beg[x] = cum;
-    cum += max(0, min(A.hq[16 * x], A.xcap) - A.hq[16 * x + 1]);
-  }
-  for (int u = (int)blockIdx.x; u < cum; u += gridDim.x) {
-    int x = kXcds - 1;
-    while (beg[x] > u) x--;
-    const HRec r = A.recs[(size_t)x * A.xcap + A.hq[16 * x + 1] + (u - beg[x])];
-    heavy_read(A, r, La, Lb, Q, threadIdx.x);
-  }
+  const int nh = *(volatile const int32_t *)A.nrecs;
+  for (int t = (int)blockIdx.x; t < nh; t += gridDim.x) heavy_read(A, A.recs[t], La, Lb, Q, threadIdx.x);
 }
 
 // Reads with count <= kCap are in their pass-1 slot; the rest in the pass-2 slot at the position of
@@ -1046,11 +930,8 @@ struct gb_fmi_reads {
   int64_t *d_offsets = nullptr;
   gb_smem *d_out = nullptr;
   int64_t out_cap = 0;
-  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow count, [2] fatal
-  gbfmi::HRec *d_recs = nullptr;  // reads handed over: kXcds queues of xcap, zeroed when allocated
-  int32_t *d_hq = nullptr;        // the queues' counters (16 ints per XCD)
-  int32_t xcap = 0;
-  int32_t epoch = 0;              // tag of the last search's records
+  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow count, [2] fatal, [4] reads handed over
+  gbfmi::HRec *d_recs = nullptr;  // reads handed over (capacity nreads); their count is d_ctl[4]
   int32_t *d_ovf_list = nullptr;
   int32_t *d_ovf_pos = nullptr;
   gb_smem *d_big = nullptr;
@@ -1353,7 +1234,6 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     if (e == hipSuccess) e = hipMalloc(&R->d_ovf_list, gbfmi::kMaxOvf * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&R->d_big, (size_t)gbfmi::kMaxOvf * gbfmi::kBigCap * sizeof(gb_smem));
     if (e == hipSuccess) e = hipMalloc(&R->d_ctl, 8 * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMalloc(&R->d_hq, 16 * gbfmi::kXcds * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&R->d_calls, 2 * sizeof(unsigned long long));
   }
   R->idx = idx;
@@ -1377,13 +1257,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   reserve(&R->d_slots, &R->cap_slots, nr * gbfmi::kCap * sizeof(gb_smem));
   reserve(&R->d_ovf_pos, &R->cap_ovf_pos, nr * sizeof(int32_t));
   reserve(&R->d_counts, &R->cap_counts, nr * sizeof(int32_t));
-  {
-    const size_t had = R->cap_heavy;
-    // a few in a hundred reads are handed over; a full queue only keeps reads in their lanes
-    R->xcap = (int32_t)std::min<size_t>(nr / 16 + 4096, (size_t)1 << 28);
-    reserve(&R->d_recs, &R->cap_heavy, (size_t)gbfmi::kXcds * R->xcap * sizeof(gbfmi::HRec));
-    if (e == hipSuccess && R->cap_heavy != had) e = hipMemset(R->d_recs, 0, R->cap_heavy);  // no tag matches
-  }
+  reserve(&R->d_recs, &R->cap_heavy, nr * sizeof(gbfmi::HRec));
   reserve(&R->d_phase, &R->cap_phase, nr * 3 * sizeof(int32_t));
   reserve(&R->d_offsets, &R->cap_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess)
@@ -1423,7 +1297,7 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
-                  (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_recs, (void *)R->d_hq})
+                  (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_recs})
     (void)hipFree(p);
   for (auto ev : R->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1471,30 +1345,14 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.budget = (budget > 0 && R->stride <= gbfmi::kHeavyMaxLen) ? budget : INT32_MAX;
     const char *pf = getenv("GB_FMI_PREFETCH");
     A.prefetch = pf && *pf == '1';
-    // GB_FMI_DRAIN: the tail hand-over's lane count (0 = off); GB_FMI_HELP=0: handed-over reads
-    // wait for smem_heavy after the kernel
-    const char *dr = getenv("GB_FMI_DRAIN");
-    const char *hp = getenv("GB_FMI_HELP");
-    const bool can = R->stride <= gbfmi::kHeavyMaxLen;  // reads the wave routine can take
-    // (tail hand-overs of ordinary reads measured no faster: the wave-per-read routine runs their
-    // forward extensions one gather at a time, and the helping waves slow the lanes still running;
-    // r03s, same box: drain 2 -> full set +1.4 %, worst 1/8 shard -0.6 %)
-    A.drain_k = can ? std::min(63, std::max(0, dr ? atoi(dr) : 0)) : 0;
-    // GB_FMI_DRAIN_CALLS: the tail hand-over's call count (0 = off); GB_FMI_LIST: the list length
-    // that hands a read over at once (0 = off)
-    const char *dc = getenv("GB_FMI_DRAIN_CALLS");
+    // GB_FMI_LIST: the list length that hands a read over at once (0 = off)
     const char *lt = getenv("GB_FMI_LIST");
-    A.drain_calls = can ? std::max(0, dc ? atoi(dc) : 0) : 0;
+    const bool can = R->stride <= gbfmi::kHeavyMaxLen;  // reads the wave routine can take
     // (list 32: full set -0.4 %, worst shard -3.7 %; 16 hands over too many ordinary reads, r03r/s)
     A.list_t = can ? std::max(0, lt ? atoi(lt) : 32) : 0;
-    A.help = can && !(hp && *hp == '0');
   }
-  if (++R->epoch <= 0) R->epoch = 1;
-  A.epoch = R->epoch;
   A.recs = R->d_recs;
-  A.hq = R->d_hq;
-  A.xcap = R->xcap;
-  GB_HIP(hipMemsetAsync(R->d_hq, 0, 16 * gbfmi::kXcds * sizeof(int32_t), R->stream));
+  A.nrecs = R->d_ctl + 4;
   A.trace = nullptr;
   if ((A.flags & 8) && R->nreads > 0) {
     const size_t bytes = (size_t)R->nreads * 3 * sizeof(int64_t);
@@ -1538,7 +1396,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
         launch(gbfmi::smem_search<false, 0>);
     }
     GB_HIP(hipGetLastError());
-    if (A.budget != INT32_MAX || A.drain_k > 0 || A.drain_calls > 0 || A.list_t > 0) {
+    if (A.budget != INT32_MAX || A.list_t > 0) {
       gbfmi::HeavyArgs H;
       H.F = A.F;
       H.qdb = A.qdb;
@@ -1547,8 +1405,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
       H.min_seed_len = A.min_seed_len;
       H.split_len = A.split_len;
       H.recs = A.recs;
-      H.hq = A.hq;
-      H.xcap = A.xcap;
+      H.nrecs = A.nrecs;
       H.slots = A.slots;
       H.big = A.big;
       H.counts = A.counts;

@@ -22,7 +22,7 @@ shards = []
 for r in range(8):
     lo, hi = shard.read_range(nreads, r, 8)
     shards.append(fmi.Reads(idx, codes[lo:hi], lens[lo:hi]))
-sets = [s for s in os.environ.get("FMI_AB", "GB_FMI_HELP=0;GB_FMI_HELP=1").split(";")]
+sets = [s for s in os.environ.get("FMI_AB", "GB_FMI_LIST=0;GB_FMI_LIST=32").split(";")]
 keys = sorted({kv.split("=")[0] for s in sets for kv in s.split(",") if kv})
 
 
