@@ -20,7 +20,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -100,26 +99,6 @@ enum State : int {
   DONE,
 };
 
-// ---- reads handed over --------------------------------------------------------------------------
-// A lane gives a read up when its forward phase leaves a long `prev` list (list_t: a repeat, whose
-// backward search the lane would extend one entry per trip) or when it has run kHeavyBudget
-// backwardExt calls (a heavy read: a few per thousand make 2.5-25x the median's calls); such a read's
-// calls cost a lane ~5 us each under load and the wave-per-read routine (heavy_read, smem_heavy after
-// the search) ~0.19 us. The read resumes there from the last position boundary its lane passed,
-// recorded in an HRec: phase `mode` (1 all positions, 2 reseeding, 3 LAST) at `pos` (x, or the
-// reseeding index), with nout SMEMs already in its slot (n1 / n2 as far as known), `calls`
-// backwardExt calls made up to there, and kb >= 0 when they are in that big slot.
-// Measured and dropped in round 3 (r03o-r03v): the search's own waves taking the records once their
-// lanes were done (inlined, the routine slowed the lane loop ~3 %; every XCD has its own L2 and they
-// are not coherent inside a kernel, so the records had to stay on the XCD that wrote them), and
-// handing over ordinary reads in the grid's tail (their forward extensions run one gather at a time
-// in the wave routine too, and the per-trip ballot slowed the search 8 %).
-constexpr int kHeavyMaxLen = 256;   // reads up to this long can be handed over (lists in LDS)
-constexpr int kHeavyBudget = 2000;  // backwardExt calls before a lane hands its read over
-struct HRec {
-  int32_t rd, mp, nout, n1, n2, calls, kb, pad;  // mp = mode << 16 | pos
-};
-
 struct SearchArgs {
   DevIndex F;
   const uint8_t *qdb;
@@ -140,114 +119,15 @@ struct SearchArgs {
   int32_t *ovf_n;
   int32_t *fatal;        // pass 2 overflow / list overflow
   unsigned long long *bwt_calls;
-  int32_t budget;        // a read still running after this many backwardExt calls is handed over to
-                         // the wave-per-read routine (heavy_read); INT32_MAX = never
-  HRec *recs;            // reads handed over (capacity nreads: a read is handed over at most once)
-  int32_t *nrecs;        // and their count
-  int32_t list_t;        // a read whose forward phase leaves a `prev` list of >= list_t entries (a
-                         // repeat: the backward search will extend them one by one) is handed over
-                         // at once (0 = never)
+  int32_t budget;        // a read still running after this many backwardExt calls is handed to the
+                         // wave-cooperative pass (smem_heavy); INT32_MAX = never
+  int32_t *heavy;        // reads handed over (capacity nreads) and their count
+  int32_t *heavy_n;
   int32_t prefetch;      // claim the next read when taking one (GB_FMI_PREFETCH, default off)
   int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof,
                          // 8 = per-read trace (start / end wall clock, backwardExt calls) into `trace`
   int64_t *trace;
 };
-
-// One handed-over read, one wave (every lane calls this with the same record): the forward and
-// LAST extensions run wave-uniform, and each backward step extends up to 64 `prev` entries at once,
-// their sequential bookkeeping as ballots (fmi_wave.h). The lists live in LDS: La, Lb of
-// kHeavyMaxLen + 1 entries, Q the read's codes. Per read the SMEM set, the per-phase counts and the
-// backwardExt count are the lane kernel's; only the order inside the read's slot may differ, which
-// sort_slots makes canonical (equal (m, n) keys are identical SMEMs). Args: SearchArgs or HeavyArgs.
-template <class Args>
-__device__ void heavy_read(const Args &A, const HRec &r, PEnt *La, PEnt *Lb, uint8_t *Q, int lane) {
-  const DevIndex &F = A.F;
-  const int rd = r.rd;
-  const int L = A.lens[rd];
-  const int mode0 = r.mp >> 16, pos0 = r.mp & 0xffff;
-  for (int i = lane; i < L; i += 64) Q[i] = A.qdb[(size_t)rd * A.stride + i];
-  __syncthreads();
-  // output slot (lane 0 writes; every lane keeps the same counters)
-  gb_smem *o = r.kb >= 0 ? A.big + (size_t)r.kb * kBigCap : A.slots + (size_t)rd * kCap;
-  int cap = r.kb >= 0 ? kBigCap : kCap, nout = r.nout;
-  bool ovf = nout > cap;
-  uint32_t calls = 0;
-  // wave-uniform: o, cap and nout are the same in every lane (the reseed loop below reads them)
-  auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
-    if (nout == cap && cap == kCap) {
-      int kb = 0;
-      if (lane == 0) kb = atomicAdd(A.ovf_n, 1);
-      kb = __shfl(kb, 0);
-      if (kb < kMaxOvf) {
-        gb_smem *big = A.big + (size_t)kb * kBigCap;
-        if (lane == 0) {
-          for (int i = 0; i < kCap; i++) big[i] = o[i];
-          A.ovf_list[kb] = rd;
-        }
-        o = big;
-        cap = kBigCap;
-      }
-    }
-    if (nout < cap) {
-      if (lane == 0) {
-        gb_smem e;
-        e.rid = (uint32_t)rd;
-        e.m = m;
-        e.n = n;
-        e.k = k;
-        e.l = l;
-        e.s = s;
-        o[nout] = e;
-      }
-    } else {
-      ovf = true;
-    }
-    nout++;
-  };
-  uint32_t *const calls_p = &calls;
-  auto one_pos = [&](int x, int min_intv) -> int {
-    return wave_one_pos(F, Q, L, x, min_intv, A.min_seed_len, La, Lb, lane, *calls_p, emit);
-  };
-  int n1 = r.n1, n2 = r.n2;
-  if (mode0 <= 1) {  // getSMEMsAllPosOneThread (min_intv 1)
-    for (int x = pos0; x < L;) x = one_pos(x, 1);
-    n1 = nout;
-  }
-  if (mode0 <= 2) {  // reseeding (fmi.cpp:293-302) over this read's phase-1 SMEMs
-    for (int ridx = mode0 == 2 ? pos0 : 0; ridx < n1 && ridx < cap; ridx++) {
-      int mm = 0, nn = 0, ss = 0;
-      if (lane == 0) {
-        const gb_smem e = o[ridx];  // (the first n of them stored by the lane that gave the read up)
-        mm = (int)e.m;
-        nn = (int)e.n;
-        ss = (int)min<int64_t>(e.s, 1 << 30);
-      }
-      mm = __shfl(mm, 0);
-      nn = __shfl(nn, 0);
-      ss = __shfl(ss, 0);
-      const int start = mm, end = nn + 1;
-      if (!(end - start < A.split_len || ss > 10)) one_pos((end + start) >> 1, ss + 1);
-    }
-    n2 = nout - n1;
-  }
-  // bwtSeedStrategyAllPosOneThread (FMI_search.cpp:1243-1326), max_intv 20; fmi.cpp passes
-  // minSeedLen + 1
-  wave_last_seeds(F, Q, L, 20, A.min_seed_len + 1, calls, emit, mode0 == 3 ? pos0 : 0);
-  if (lane == 0) {
-    const uint32_t total = (uint32_t)r.calls + calls;
-    A.counts[rd] = nout;
-    A.phase[3 * rd + 0] = n1;
-    A.phase[3 * rd + 1] = n2;
-    A.phase[3 * rd + 2] = nout - n1 - n2;
-    atomicAdd(A.bwt_calls, (unsigned long long)total);
-    if (ovf) atomicAdd(A.fatal, 1);
-    if (A.trace) {  // the start was stamped by the lane that took the read
-      A.trace[3 * (size_t)rd + 1] = (int64_t)wall_clock64();
-      A.trace[3 * (size_t)rd + 2] = -(int64_t)total;  // negative: finished by a wave
-    }
-  }
-  __syncthreads();
-}
 
 // Diagnostic phase clocks (GB_FMI_FLAGS & 4): per-wave s_memtime sums of [state machine, gather
 // wait, consume] and the trip count; read with gb_fmi_debug_prof().
@@ -392,10 +272,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     }
     nout++;
   };
-  // the last position boundary this lane passed (see HRec): where a handed-over read resumes
-  int b_mode = 1, b_pos = 0, b_nout = 0;
-  uint32_t b_calls = 0;
-  bool long_list = false;  // list_t reached (see SearchArgs::list_t)
 
   const bool prof = A.flags & 4;
   int64_t t_read = 0;
@@ -407,23 +283,13 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   bool pend = false;
   while (true) {
     const unsigned long long tA = prof ? clock64() : 0;
-    // hand the read over (see HRec): a long list or a heavy read
-    if ((calls_read >= (uint32_t)A.budget || long_list) && st != NEXT_READ && st != DONE && st != FINISH) {
-      // what it did after the boundary is dropped (those calls are not counted; the resumed read
-      // counts the ones up to it); a big slot it took after the boundary is released
-      const int kb = kb_cur >= 0 && b_nout > kCap ? kb_cur : -1;
-      if (kb_cur >= 0 && kb < 0) A.ovf_list[kb_cur] = -1;
-      HRec hr;
-      hr.rd = rd;
-      hr.mp = (b_mode << 16) | b_pos;
-      hr.nout = b_nout;
-      hr.n1 = n1;
-      hr.n2 = n2;
-      hr.calls = (int32_t)b_calls;
-      hr.kb = kb;
-      hr.pad = 0;
-      A.recs[atomicAdd(A.nrecs, 1)] = hr;
-      if (A.flags & 8) A.trace[3 * (size_t)rd] = t_read;
+    if (calls_read >= (uint32_t)A.budget && st != NEXT_READ && st != DONE) {
+      // a heavy read (a few per thousand, up to ~25x the median's backwardExt calls in repeats)
+      // would hold its wave, and at the end of the grid the whole step, for its full length: drop
+      // what it did (its calls are not counted, a big slot it took is released) and hand it to
+      // smem_heavy, which spreads each backward step's independent extensions over a wave
+      if (kb_cur >= 0) A.ovf_list[kb_cur] = -1;
+      A.heavy[atomicAdd(A.heavy_n, 1)] = rd;
       pend = false;
       st = NEXT_READ;
     }
@@ -468,7 +334,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           nout = 0;
           ovf = false;
           calls_read = 0;
-          long_list = false;
           mode = 1;
           x = 0;
           min_intv = 1;
@@ -476,12 +341,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           break;
         }
         case OP_START:
-          if (mode == 1) {
-            b_mode = 1;
-            b_pos = x;
-            b_nout = nout;
-            b_calls = calls_read;
-          }
           if (mode == 1 && x >= L) {  // getSMEMsAllPosOneThread done: reseed next
             n1 = nout;
             ridx = 0;
@@ -531,7 +390,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           tc = numPrev - 1;
           j = x - 1;
           st = BWD_ITER;
-          if (A.list_t > 0 && numPrev >= A.list_t) long_list = true;
           break;
         case BWD_ITER:
           if (j < 0) {
@@ -589,10 +447,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
         case P2_NEXT: {
           // fmi.cpp:293-302: SMEMs of length >= split_len with s <= splitWidth(10) restart at
           // the midpoint with min_intv = s + 1
-          b_mode = 2;
-          b_pos = ridx;
-          b_nout = nout;
-          b_calls = calls_read;
           bool found = false;
           while (ridx < n1 && ridx < cap) {
             const gb_smem e = o[ridx];
@@ -616,10 +470,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           break;
         }
         case P3_X:
-          b_mode = 3;
-          b_pos = x;
-          b_nout = nout;
-          b_calls = calls_read;
           if (x >= L) {
             st = FINISH;
             break;
@@ -805,14 +655,37 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   }
 }
 
-// ---- handed-over reads left after smem_search (all of them when its waves do not take any) ------
+// ---- heavy reads: one wave per read ------------------------------------------------------------
+// In a repeat a read's `prev` lists grow long and its backward search makes numPrev extensions per
+// position j (FMI_search.cpp:1103-1160): a few reads per thousand make 2.5-25x the median's calls.
+// Those extensions are independent of each other -- only the bookkeeping after them is sequential
+// -- so here a wave takes one read: the forward and LAST extensions run wave-uniform (every lane
+// computes the same one), each backward step extends up to 64 list entries at once, and the
+// reference's sequential scan over the results becomes ballots:
+//   * the first loop stops at the first entry f with s' >= min_intv (push) or with s' < min_intv and
+//     a long enough SMEM (emit it);
+//   * from f on, an entry with s' >= min_intv is pushed iff its s' differs from curr_s, the s' of
+//     the last push -- which is always the s' of the previous entry with s' >= min_intv (an entry
+//     not pushed had the same s' as that push), so the test is against the nearest lower such lane.
+// The lists live in LDS (reads up to kHeavyMaxLen bases). Per read the SMEM set, the per-phase
+// counts and the backwardExt count are the lane kernel's; only the order inside the read's slot
+// differs, which sort_slots makes canonical (equal (m, n) keys are identical SMEMs).
+// Measured and dropped in round 3 (r03o-r03w, same-box A/B against this version): resuming a
+// handed-over read from its last position boundary instead of from scratch, with a list-length
+// trigger; the search's own waves taking handed-over reads once their lanes were done (each XCD has
+// its own L2, not coherent with the others inside a kernel, so the records had to stay per XCD); and
+// handing over ordinary reads in the grid's tail. The extra state in the lane loop cost more
+// (3-12 %) than the post-pass time they saved.
+constexpr int kHeavyMaxLen = 256;
+constexpr int kHeavyBudget = 2000;  // backwardExt calls before a lane hands its read over
+
 struct HeavyArgs {
   DevIndex F;
   const uint8_t *qdb;
   const int32_t *lens;
   int32_t stride, min_seed_len, split_len;
-  const HRec *recs;  // as SearchArgs
-  const int32_t *nrecs;
+  const int32_t *heavy;
+  const int32_t *heavy_n;
   gb_smem *slots;  // kCap per read
   gb_smem *big;
   int32_t *counts, *phase, *ovf_list, *ovf_n, *fatal;
@@ -823,8 +696,94 @@ struct HeavyArgs {
 __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
   __shared__ PEnt La[kHeavyMaxLen + 1], Lb[kHeavyMaxLen + 1];
   __shared__ uint8_t Q[kHeavyMaxLen];
-  const int nh = *(volatile const int32_t *)A.nrecs;
-  for (int t = (int)blockIdx.x; t < nh; t += gridDim.x) heavy_read(A, A.recs[t], La, Lb, Q, threadIdx.x);
+  const DevIndex F = A.F;
+  const int lane = threadIdx.x;
+  const int nh = *(volatile const int32_t *)A.heavy_n;
+  for (int t = blockIdx.x; t < nh; t += gridDim.x) {
+    const int rd = A.heavy[t];
+    const int L = A.lens[rd];
+    const int64_t t_read = A.trace ? (int64_t)wall_clock64() : 0;
+    for (int i = lane; i < L; i += 64) Q[i] = A.qdb[(size_t)rd * A.stride + i];
+    __syncthreads();
+    // ---- output slot (lane 0 writes; every lane keeps the same counters) ----------------------
+    gb_smem *o = A.slots + (size_t)rd * kCap;
+    int cap = kCap, nout = 0;
+    bool ovf = false;
+    uint32_t calls = 0;
+    // wave-uniform: o, cap and nout are the same in every lane (the reseed loop below reads them)
+    auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
+      if (nout == cap && cap == kCap) {
+        int kb = 0;
+        if (lane == 0) kb = atomicAdd(A.ovf_n, 1);
+        kb = __shfl(kb, 0);
+        if (kb < kMaxOvf) {
+          gb_smem *big = A.big + (size_t)kb * kBigCap;
+          if (lane == 0) {
+            for (int i = 0; i < kCap; i++) big[i] = o[i];
+            A.ovf_list[kb] = rd;
+          }
+          o = big;
+          cap = kBigCap;
+        }
+      }
+      if (nout < cap) {
+        if (lane == 0) {
+          gb_smem e;
+          e.rid = (uint32_t)rd;
+          e.m = m;
+          e.n = n;
+          e.k = k;
+          e.l = l;
+          e.s = s;
+          o[nout] = e;
+        }
+      } else {
+        ovf = true;
+      }
+      nout++;
+    };
+
+    uint32_t *const calls_p = &calls;
+    auto one_pos = [&](int x, int min_intv) -> int {
+      return wave_one_pos(F, Q, L, x, min_intv, A.min_seed_len, La, Lb, lane, *calls_p, emit);
+    };
+
+    // getSMEMsAllPosOneThread (min_intv 1)
+    for (int x = 0; x < L;) x = one_pos(x, 1);
+    const int n1 = nout;
+    // reseeding (fmi.cpp:293-302) over this read's phase-1 SMEMs
+    for (int ridx = 0; ridx < n1 && ridx < cap; ridx++) {
+      int mm = 0, nn = 0, ss = 0;
+      if (lane == 0) {
+        const gb_smem e = o[ridx];
+        mm = (int)e.m;
+        nn = (int)e.n;
+        ss = (int)min<int64_t>(e.s, 1 << 30);
+      }
+      mm = __shfl(mm, 0);
+      nn = __shfl(nn, 0);
+      ss = __shfl(ss, 0);
+      const int start = mm, end = nn + 1;
+      if (!(end - start < A.split_len || ss > 10)) one_pos((end + start) >> 1, ss + 1);
+    }
+    const int n2 = nout - n1;
+    // bwtSeedStrategyAllPosOneThread (FMI_search.cpp:1243-1326), max_intv 20
+    wave_last_seeds(F, Q, L, 20, A.min_seed_len + 1, calls, emit);  // fmi.cpp passes minSeedLen + 1
+    if (lane == 0) {
+      A.counts[rd] = nout;
+      A.phase[3 * rd + 0] = n1;
+      A.phase[3 * rd + 1] = n2;
+      A.phase[3 * rd + 2] = nout - n1 - n2;
+      atomicAdd(A.bwt_calls, (unsigned long long)calls);
+      if (ovf) atomicAdd(A.fatal, 1);
+      if (A.trace) {
+        A.trace[3 * (size_t)rd] = t_read;
+        A.trace[3 * (size_t)rd + 1] = (int64_t)wall_clock64();
+        A.trace[3 * (size_t)rd + 2] = -(int64_t)calls;  // negative: done by smem_heavy
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // Reads with count <= kCap are in their pass-1 slot; the rest in the pass-2 slot at the position of
@@ -930,8 +889,8 @@ struct gb_fmi_reads {
   int64_t *d_offsets = nullptr;
   gb_smem *d_out = nullptr;
   int64_t out_cap = 0;
-  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow count, [2] fatal, [4] reads handed over
-  gbfmi::HRec *d_recs = nullptr;  // reads handed over (capacity nreads); their count is d_ctl[4]
+  int32_t *d_ctl = nullptr;  // [0] next_read, [1] overflow count, [2] fatal, [3] unused, [4] heavy reads
+  int32_t *d_heavy = nullptr;  // reads handed to smem_heavy (capacity nreads)
   int32_t *d_ovf_list = nullptr;
   int32_t *d_ovf_pos = nullptr;
   gb_smem *d_big = nullptr;
@@ -1257,7 +1216,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   reserve(&R->d_slots, &R->cap_slots, nr * gbfmi::kCap * sizeof(gb_smem));
   reserve(&R->d_ovf_pos, &R->cap_ovf_pos, nr * sizeof(int32_t));
   reserve(&R->d_counts, &R->cap_counts, nr * sizeof(int32_t));
-  reserve(&R->d_recs, &R->cap_heavy, nr * sizeof(gbfmi::HRec));
+  reserve(&R->d_heavy, &R->cap_heavy, nr * sizeof(int32_t));
   reserve(&R->d_phase, &R->cap_phase, nr * 3 * sizeof(int32_t));
   reserve(&R->d_offsets, &R->cap_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess)
@@ -1297,7 +1256,7 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
   for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
-                  (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_recs})
+                  (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_heavy})
     (void)hipFree(p);
   for (auto ev : R->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -1345,14 +1304,9 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.budget = (budget > 0 && R->stride <= gbfmi::kHeavyMaxLen) ? budget : INT32_MAX;
     const char *pf = getenv("GB_FMI_PREFETCH");
     A.prefetch = pf && *pf == '1';
-    // GB_FMI_LIST: the list length that hands a read over at once (0 = off)
-    const char *lt = getenv("GB_FMI_LIST");
-    const bool can = R->stride <= gbfmi::kHeavyMaxLen;  // reads the wave routine can take
-    // (list 32: full set -0.4 %, worst shard -3.7 %; 16 hands over too many ordinary reads, r03r/s)
-    A.list_t = can ? std::max(0, lt ? atoi(lt) : 32) : 0;
   }
-  A.recs = R->d_recs;
-  A.nrecs = R->d_ctl + 4;
+  A.heavy = R->d_heavy;
+  A.heavy_n = R->d_ctl + 4;
   A.trace = nullptr;
   if ((A.flags & 8) && R->nreads > 0) {
     const size_t bytes = (size_t)R->nreads * 3 * sizeof(int64_t);
@@ -1396,7 +1350,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
         launch(gbfmi::smem_search<false, 0>);
     }
     GB_HIP(hipGetLastError());
-    if (A.budget != INT32_MAX || A.list_t > 0) {
+    if (A.budget != INT32_MAX) {
       gbfmi::HeavyArgs H;
       H.F = A.F;
       H.qdb = A.qdb;
@@ -1404,8 +1358,8 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
       H.stride = A.stride;
       H.min_seed_len = A.min_seed_len;
       H.split_len = A.split_len;
-      H.recs = A.recs;
-      H.nrecs = A.nrecs;
+      H.heavy = A.heavy;
+      H.heavy_n = A.heavy_n;
       H.slots = A.slots;
       H.big = A.big;
       H.counts = A.counts;
@@ -1415,8 +1369,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
       H.fatal = A.fatal;
       H.bwt_calls = A.bwt_calls;
       H.trace = A.trace;
-      // what the search's waves left (nothing when they take the records themselves); the count is
-      // on the device: a grid of 16 waves per CU strides over the list
+      // the heavy-read count is on the device: a grid of 16 waves per CU strides over the list
       hipLaunchKernelGGL(gbfmi::smem_heavy, dim3((unsigned)std::max(1, R->lanes / 64 * 16 / 12)), dim3(64), 0,
                          R->stream, H);
       GB_HIP(hipGetLastError());

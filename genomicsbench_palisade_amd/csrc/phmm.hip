@@ -493,286 +493,6 @@ __device__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, c
   return na;
 }
 
-// ---- f32 pass, two stacks per wave (round 3) --------------------------------------------------
-// The recurrence's 8 multiplies and 4 adds per cell (no FMA) run as packed pairs: v_pk_mul_f32 /
-// v_pk_add_f32 compute two f32 elements per lane per instruction, each rounded as the scalar op, so
-// every cell stays bit-identical. A wave sweeps two stacks at once -- stack A in the low and stack B
-// in the high element of every register pair (adjacent stacks of the LPT order: similar cost) --
-// while the DPP shifts, the dist select and the LDS reads stay per stack. Per two cells a step
-// issues ~22 VALU instead of 2 x 16, and the boundary records of both stacks are one 16-byte LDS
-// record per column. Each half runs phmm_stack's logic for its own stack (own haplotype codes and
-// length C; the half whose stack is shorter sweeps on through zero-filled columns).
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct __attribute__((aligned(16))) Brec2 {
-  f2 z, w;  // .x: stack A, .y: stack B (Brec's z / w)
-};
-struct __attribute__((aligned(16))) StackPair {
-  Stack a, b;  // b.count == 0: no second stack
-};
-struct RowParams2 {
-  f2 pMY, pYY, dmatch, dmis, nMM, nGAPM, nGAPMx, nMX, nXX;
-  uint32_t rmA, rmB;
-};
-struct LaneState2 {
-  f2 Mp, Yp, zo, wo, zd;
-};
-
-// dist select from a code offset: v_bfe_i32 gives the lane's 0 / -1 mask, v_bfi_b32 picks the bits
-__device__ __forceinline__ float select_bfi(uint32_t rmask, uint32_t h, float dmatch, float dmis) {
-  uint32_t m, r;
-  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(rmask), "v"(h));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(__builtin_bit_cast(uint32_t, dmatch)),
-      "v"(__builtin_bit_cast(uint32_t, dmis)));
-  return __builtin_bit_cast(float, r);
-}
-
-template <bool kSum, bool kWrite>
-__device__ __forceinline__ void phmm_step2(const Brec2 &rec, uint32_t hA, uint32_t hB, LaneState2 &st,
-                                           const RowParams2 &P, f2 &sumM, f2 &sumX, Brec2 *wr, bool last_lane) {
-  f2 X, zdn, dist;
-  X.x = dpp<dpp_shr>(st.wo.x, rec.w.x);  // X[r][c]
-  X.y = dpp<dpp_shr>(st.wo.y, rec.w.y);
-  zdn.x = dpp<dpp_shr>(st.zo.x, rec.z.x);  // bracket for column c+1
-  zdn.y = dpp<dpp_shr>(st.zo.y, rec.z.y);
-  dist.x = select_bfi(P.rmA, hA, P.dmatch.x, P.dmis.x);
-  dist.y = select_bfi(P.rmB, hB, P.dmatch.y, P.dmis.y);
-  const f2 M = st.zd * dist;
-  const f2 Y = st.Mp * P.pMY + st.Yp * P.pYY;
-  st.zo = (M * P.nMM + X * P.nGAPMx) + Y * P.nGAPM;
-  st.wo = M * P.nMX + X * P.nXX;
-  if constexpr (kSum) {
-    sumM = sumM + M;
-    sumX = sumX + X;
-  }
-  if constexpr (kWrite) {
-    if (last_lane) {
-      Brec2 b;
-      b.z = st.zo;
-      b.w = st.wo;
-      *wr = b;
-    }
-  }
-  st.zd = zdn;
-  st.Mp = M;
-  st.Yp = Y;
-}
-
-// phmm_stripe for a pair: the rows in lmA / lmB are testcases' last rows of stack A / B, whose sums
-// lane k stores at step C + k - 1 of its own stack (outA / outB: the lane's own result slots).
-template <bool kSum, bool kWrite>
-__device__ __forceinline__ void phmm_stripe2(int steps, LaneState2 &st, const RowParams2 &P, f2 &sumM, f2 &sumX,
-                                             Brec2 *__restrict__ bnd, const uint8_t *__restrict__ hcA,
-                                             const uint8_t *__restrict__ hcB, int CA, int CB, int lane,
-                                             uint64_t lmA, uint64_t lmB, float *outA, float *outB) {
-  const uint8_t *hla = hcA + 1 - lane, *hlb = hcB + 1 - lane;
-  const bool last_lane = lane == kWave - 1;
-  constexpr int U = 4;
-  constexpr int kNoWrite = 60;  // as phmm_stripe
-  uint64_t pa = lmA, pb = lmB;
-  int ta = (kSum && pa) ? CA + __builtin_ctzll(pa) - 1 : INT_MAX;
-  int tb = (kSum && pb) ? CB + __builtin_ctzll(pb) - 1 : INT_MAX;
-  auto single = [&](int tt, auto wr_tag) {
-    constexpr bool W = decltype(wr_tag)::value;
-    phmm_step2<kSum, W>(bnd[tt + 1], hla[tt], hlb[tt], st, P, sumM, sumX, bnd + (tt - (kWave - 2)), last_lane);
-    if (kSum && tt == ta) {
-      if (lane == __builtin_ctzll(pa)) *outA = sumM.x + sumX.x;
-      pa &= pa - 1;
-      ta = pa ? CA + __builtin_ctzll(pa) - 1 : INT_MAX;
-    }
-    if (kSum && tt == tb) {
-      if (lane == __builtin_ctzll(pb)) *outB = sumM.y + sumX.y;
-      pb &= pb - 1;
-      tb = pb ? CB + __builtin_ctzll(pb) - 1 : INT_MAX;
-    }
-  };
-  int vzero;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-  Brec2 *wb = bnd - (kWave - 2) + vzero;
-  auto run = [&](int t, int end, auto wr_tag) {
-    constexpr bool W = decltype(wr_tag)::value;
-    for (; t + U <= end; t += U) {
-      if (kSum && min(ta, tb) < t + U) {
-        for (int u = 0; u < U; u++) single(t + u, wr_tag);
-        continue;
-      }
-      Brec2 *wr = wb + t;
-      const Brec2 c0 = wr[kWave - 1], c1 = wr[kWave], c2 = wr[kWave + 1], c3 = wr[kWave + 2];
-      const uint32_t a0 = hla[t], a1 = hla[t + 1], a2 = hla[t + 2], a3 = hla[t + 3];
-      const uint32_t b0 = hlb[t], b1 = hlb[t + 1], b2 = hlb[t + 2], b3 = hlb[t + 3];
-      phmm_step2<kSum, W>(c0, a0, b0, st, P, sumM, sumX, wr, last_lane);
-      phmm_step2<kSum, W>(c1, a1, b1, st, P, sumM, sumX, wr + 1, last_lane);
-      phmm_step2<kSum, W>(c2, a2, b2, st, P, sumM, sumX, wr + 2, last_lane);
-      phmm_step2<kSum, W>(c3, a3, b3, st, P, sumM, sumX, wr + 3, last_lane);
-    }
-    for (; t < end; t++) single(t, wr_tag);
-  };
-  if constexpr (kWrite) {
-    const int a = min(steps, kNoWrite);
-    run(0, a, std::false_type{});
-    run(a, steps, std::true_type{});
-  } else {
-    run(0, steps, std::false_type{});
-  }
-}
-
-// One stack's per-wave view for the pair kernel (f32: every testcase is computed, so lane a holds
-// entry a without compaction).
-struct Half {
-  int C, T_rows, e_start, e_R;
-  uint32_t e_read, e_out;
-  float init_Y;
-};
-
-__device__ __forceinline__ Half half_init(const Stack &S, const uint32_t *__restrict__ stk_tc,
-                                          const TcDesc *__restrict__ descs, float init_const, int lane) {
-  Half H;
-  H.C = (int)S.C;
-  TcDesc d = {0, 0, 0, 0};
-  if (lane < (int)S.count) d = descs[stk_tc[S.first + lane]];
-  const int rows = lane < (int)S.count ? (int)(d.dims & 0xffff) + 2 : 0;
-  const int incl = scan_add(rows);
-  H.T_rows = __builtin_amdgcn_readlane(incl, 63);
-  H.e_start = incl - rows;
-  H.e_R = rows - 2;
-  H.e_read = d.read_off;
-  H.e_out = d.out_idx;
-  H.init_Y = S.count ? init_const / (float)max(H.C, 1) : 0.f;
-  return H;
-}
-
-// The lane's row of stripe s of one stack (phmm_stack's per-stripe setup: va, v0, read rows, dead
-// lanes beyond the stack), as the scalar RowParams / LaneState of that stack.
-__device__ __forceinline__ void half_row(const Half &H, int na, int s, int lane, const uint8_t *__restrict__ pool,
-                                         const DevTab<float> &tab, float bnd0z, RowParams<float> &P,
-                                         LaneState<float> &st, bool &last_row, uint32_t &out_idx) {
-  const int g = s * kWave + lane;
-  int lo = 0, hi = na - 1;
-  while (__builtin_amdgcn_ballot_w64(lo < hi)) {
-    const int mid = (lo + hi + 1) >> 1;
-    const int sm = __shfl(H.e_start, mid);
-    if (lo < hi) {
-      if (sm <= g) lo = mid; else hi = mid - 1;
-    }
-  }
-  const int e_start = __shfl(H.e_start, lo), e_R = __shfl(H.e_R, lo);
-  const uint32_t e_read = (uint32_t)__shfl((int)H.e_read, lo);
-  out_idx = (uint32_t)__shfl((int)H.e_out, lo);
-  const int r = g - e_start;
-  const bool dead = na == 0 || g >= H.T_rows;
-  const uint8_t *rbase = pool + e_read;
-  st.Mp = st.zo = st.wo = 0.f;
-  st.Yp = 0.f;
-  st.zd = lane == 0 ? bnd0z : 0.f;
-  float pMM, pGAPM, pMX, pXX, a, b, dm, dx;
-  uint32_t f;
-  const float zero = 0.f, one = 1.f;
-  P.nMM = P.nGAPM = P.nGAPMx = P.nMX = P.nXX = zero;
-  if (dead) {
-    P.pMY = P.pYY = P.dmatch = P.dmis = zero;
-    P.rmask = 0;
-  } else if (r == 0) {  // va
-    P.pMY = zero;
-    P.pYY = one;
-    P.dmatch = P.dmis = zero;
-    P.rmask = 0;
-    P.nGAPM = one;
-    st.Yp = H.init_Y;
-    st.zo = (zero * zero + zero * zero) + H.init_Y * one;
-  } else if (r == 1) {  // v0
-    P.pMY = P.pYY = zero;
-    P.dmatch = one;
-    P.dmis = zero;
-    P.rmask = 0x3F;
-    load_row(rbase, e_R, 0, tab, pMM, pGAPM, pMX, pXX, a, b, dm, dx, f);
-    P.nMM = pGAPM;
-    st.zd = H.init_Y;
-    if (lane == 0) st.zo = (H.init_Y * P.nMM + zero * zero) + zero * zero;
-  } else {
-    load_row(rbase, e_R, r - 2, tab, pMM, pGAPM, pMX, pXX, P.pMY, P.pYY, P.dmatch, P.dmis, P.rmask);
-    if (r - 1 < e_R) {
-      load_row(rbase, e_R, r - 1, tab, P.nMM, P.nGAPM, P.nMX, P.nXX, a, b, dm, dx, f);
-      P.nGAPMx = P.nGAPM;
-    }
-  }
-  last_row = !dead && r == e_R + 1;
-}
-
-__global__ __launch_bounds__(64) void phmm_forward_pair(const StackPair *__restrict__ pairs,
-                                                        const uint32_t *__restrict__ stk_tc,
-                                                        const TcDesc *__restrict__ descs,
-                                                        const uint8_t *__restrict__ pool, DevTab<float> tab,
-                                                        float *__restrict__ raw_out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  const StackPair SP = pairs[blockIdx.x];
-  const int lane = threadIdx.x;
-  const Half A = half_init(SP.a, stk_tc, descs, tab.init_const, lane);
-  const Half B = half_init(SP.b, stk_tc, descs, tab.init_const, lane);
-  const int nA = (int)SP.a.count, nB = (int)SP.b.count;
-  const int Cm = max(A.C, B.C);
-  // LDS: the pair's records for columns [-kRecPad, Cm+kBndPad), then each stack's codes for columns
-  // [-kWave, Cm+kBndPad) (zero beyond its own C)
-  Brec2 *bnd = reinterpret_cast<Brec2 *>(smem_raw) + kRecPad;
-  const int ncode = Cm + kBndPad + kWave;
-  uint8_t *hcA = smem_raw + sizeof(Brec2) * (size_t)(Cm + kBndPad + kRecPad) + kWave;
-  uint8_t *hcB = hcA + ncode;
-  const uint8_t *codeA = pool + SP.a.hap_off, *codeB = pool + SP.b.hap_off;
-  for (int c = lane; c < Cm + kBndPad; c += kWave) {
-    Brec2 z;
-    z.z = 0.f;
-    z.w = 0.f;
-    bnd[c] = z;
-  }
-  for (int c = lane - kWave; c < Cm + kBndPad; c += kWave) {
-    hcA[c] = (c >= 1 && c <= A.C) ? codeA[c - 1] : (c == 0 ? 5 : (c < 0 ? 6 : 0));
-    hcB[c] = (nB && c >= 1 && c <= B.C) ? codeB[c - 1] : (c == 0 ? 5 : (c < 0 ? 6 : 0));
-  }
-  __syncthreads();
-  const int sA = (A.T_rows + kWave - 1) / kWave, sB = nB ? (B.T_rows + kWave - 1) / kWave : 0;
-  const int nstripes = max(sA, sB);
-  for (int s = 0; s < nstripes; s++) {
-    RowParams<float> pa, pb;
-    LaneState<float> qa, qb;
-    bool la, lb;
-    uint32_t oa, ob;
-    half_row(A, s < sA ? nA : 0, s, lane, pool, tab, bnd[0].z.x, pa, qa, la, oa);
-    half_row(B, s < sB ? nB : 0, s, lane, pool, tab, bnd[0].z.y, pb, qb, lb, ob);
-    RowParams2 P;
-    P.pMY = f2{pa.pMY, pb.pMY};
-    P.pYY = f2{pa.pYY, pb.pYY};
-    P.dmatch = f2{pa.dmatch, pb.dmatch};
-    P.dmis = f2{pa.dmis, pb.dmis};
-    P.nMM = f2{pa.nMM, pb.nMM};
-    P.nGAPM = f2{pa.nGAPM, pb.nGAPM};
-    P.nGAPMx = f2{pa.nGAPMx, pb.nGAPMx};
-    P.nMX = f2{pa.nMX, pb.nMX};
-    P.nXX = f2{pa.nXX, pb.nXX};
-    P.rmA = pa.rmask;
-    P.rmB = pb.rmask;
-    LaneState2 st;
-    st.Mp = f2{qa.Mp, qb.Mp};
-    st.Yp = f2{qa.Yp, qb.Yp};
-    st.zo = f2{qa.zo, qb.zo};
-    st.wo = f2{qa.wo, qb.wo};
-    st.zd = f2{qa.zd, qb.zd};
-    const uint64_t lmA = __builtin_amdgcn_ballot_w64(la), lmB = __builtin_amdgcn_ballot_w64(lb);
-    const int stA = s < sA ? (s < sA - 1 ? A.C + kWave - 1 : A.C + (A.T_rows - s * kWave) - 1) : 0;
-    const int stB = s < sB ? (s < sB - 1 ? B.C + kWave - 1 : B.C + (B.T_rows - s * kWave) - 1) : 0;
-    const int steps = max(stA, stB);
-    const bool more = s < nstripes - 1;
-    f2 sumM = 0.f, sumX = 0.f;
-    float *outA = raw_out + oa, *outB = raw_out + ob;
-    if (lmA | lmB) {
-      if (more)
-        phmm_stripe2<true, true>(steps, st, P, sumM, sumX, bnd, hcA, hcB, A.C, B.C, lane, lmA, lmB, outA, outB);
-      else
-        phmm_stripe2<true, false>(steps, st, P, sumM, sumX, bnd, hcA, hcB, A.C, B.C, lane, lmA, lmB, outA, outB);
-    } else {
-      phmm_stripe2<false, true>(steps, st, P, sumM, sumX, bnd, hcA, hcB, A.C, B.C, lane, 0, 0, outA, outB);
-    }
-    __syncthreads();
-  }
-}
-
 // f32 pass: one stack per workgroup (LPT order). f64 pass: a persistent grid takes stacks through
 // counter[1] and recomputes their testcases whose f32 result fell below MIN_ACCEPTED; counter[0]
 // counts them.
@@ -928,8 +648,6 @@ struct gb_phmm_batch {
   uint32_t *d_stk_tc = nullptr;  // testcase indices, stack by stack
   Stack *d_stacks = nullptr;     // LPT order
   int nstacks = 0;
-  StackPair *d_pairs = nullptr;  // the f32 pass: adjacent stacks of the LPT order, two per wave
-  int npairs = 0;
   int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
@@ -1163,12 +881,6 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     for (size_t c = 1; c < at.size(); c++) at[c] += at[c - 1];
     for (size_t k = 0; k < stacks.size(); k++) sorted_stacks[at[(size_t)(cmax - scost[k])]++] = stacks[k];
   }
-  // the f32 pass's pairs: stacks 2w and 2w+1 of the LPT order (similar cost), the last one alone
-  std::vector<StackPair> pairs((sorted_stacks.size() + 1) / 2);
-  for (size_t w = 0; w < pairs.size(); w++) {
-    pairs[w].a = sorted_stacks[2 * w];
-    pairs[w].b = 2 * w + 1 < sorted_stacks.size() ? sorted_stacks[2 * w + 1] : Stack{0, 0, 0, 0};
-  }
   std::vector<uint32_t> stk_tc(order.begin(), order.end());
   if (pool.empty()) pool.resize(4);
   pool.resize((pool.size() + 15) & ~size_t(15));
@@ -1177,9 +889,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   const size_t nn = std::max(n, 1);
   if (nn > b->cap_n) {
     for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
-                    (void *)b->d_stacks, (void *)b->d_pairs})
+                    (void *)b->d_stacks})
       (void)hipFree(p);
-    b->d_pairs = nullptr;
     b->d_desc = nullptr;
     b->d_rf = nullptr;
     b->d_rd = b->d_out = nullptr;
@@ -1192,7 +903,6 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
     GB_HIP(hipMalloc(&b->d_stk_tc, sizeof(uint32_t) * nn));
     GB_HIP(hipMalloc(&b->d_stacks, sizeof(Stack) * nn));  // at most one stack per testcase
-    GB_HIP(hipMalloc(&b->d_pairs, sizeof(StackPair) * (nn / 2 + 1)));
     b->cap_n = nn;
   }
   if (pool.size() > b->cap_pool) {
@@ -1208,15 +918,12 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     GB_HIP(hipMemcpyAsync(b->d_stk_tc, stk_tc.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
     GB_HIP(hipMemcpyAsync(b->d_stacks, sorted_stacks.data(), sizeof(Stack) * sorted_stacks.size(),
                           hipMemcpyHostToDevice, b->stream));
-    GB_HIP(hipMemcpyAsync(b->d_pairs, pairs.data(), sizeof(StackPair) * pairs.size(), hipMemcpyHostToDevice,
-                          b->stream));
   }
   GB_HIP(hipMemcpyAsync(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice, b->stream));
   GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
   clk.mark("upload");
   b->n = n;
   b->nstacks = (int)sorted_stacks.size();
-  b->npairs = (int)pairs.size();
   b->max_haplen = max_h;
   b->cells = cells;
   b->ran = false;
@@ -1291,21 +998,14 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   if (n > 0) {
     const size_t rec = (size_t)(b->max_haplen + kBndPad + kRecPad), codes = (size_t)(b->max_haplen + kBndPad + kWave);
     const size_t lds_f = sizeof(Brec<float>) * rec + codes + 16;
-    const size_t lds_p = sizeof(Brec2) * rec + 2 * codes + 16;
     const size_t lds_d = sizeof(Brec<double>) * rec + codes + 16;
     auto f32k = phmm_forward<float, false>;
     auto f64k = phmm_forward<double, true>;
     const int ns = b->nstacks;
     if (!b->force_f64) {
-      // GB_PHMM_PAIR=0: one stack per wave (the round-2 f32 kernel), for A/B runs
-      const char *pe = getenv("GB_PHMM_PAIR");
-      if ((pe && *pe == '0') || lds_p > 160 * 1024)  // (haplotypes over ~8.4 k columns: single stacks)
-        hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
-                           b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
-                           b->d_count, 0);
-      else
-        hipLaunchKernelGGL(phmm_forward_pair, dim3(b->npairs), dim3(kWave), lds_p, b->stream, b->d_pairs, b->d_stk_tc,
-                           b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf);
+      hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
+                         b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
+                         b->d_count, 0);
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
@@ -1412,7 +1112,6 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   (void)hipFree(b->d_out);
   (void)hipFree(b->d_stk_tc);
   (void)hipFree(b->d_stacks);
-  (void)hipFree(b->d_pairs);
   (void)hipFree(b->d_count);
   for (auto e : b->ev)
     if (e) (void)hipEventDestroy(e);

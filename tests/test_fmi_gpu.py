@@ -123,19 +123,15 @@ def test_overflow_second_pass(fmi):
     assert rs.timing()[2] == oi.bwt_calls()
 
 
-@pytest.mark.parametrize("budget,min_seed,rep,lst", [
-    ("1", 19, 0.3, "32"), ("150", 19, 0.3, "32"), ("700", 19, 0.4, "32"), ("60", 6, 0.3, "32"),
-    ("0", 19, 0.3, "0"), ("0", 19, 0.3, "2"), ("150", 19, 0.3, "4"), ("60", 6, 0.3, "3"), ("2000", 19, 0.4, "8")])
-def test_heavy_read_pass_exact(fmi, monkeypatch, budget, min_seed, rep, lst):
-    """Reads the lane kernel hands over -- after GB_FMI_HEAVY backwardExt calls, or when a forward
-    phase leaves a `prev` list of GB_FMI_LIST entries or more -- resume in smem_heavy, one wave per
-    read (64 prev-list extensions per backward step), from the last position boundary their lane
-    passed. With small budgets and list lengths most reads take that path, from every phase --
-    including reads promoted to big slots before or after the boundary (min_seed_len 6) and reads
-    longer than 64 bases' lists -- and the SMEM lists, per-batch and per-phase counts and
-    backwardExt calls stay those of the oracle. Budget 0 with list 0 = never hand over."""
+@pytest.mark.parametrize("budget,min_seed,rep", [("1", 19, 0.3), ("150", 19, 0.3), ("700", 19, 0.4),
+                                                  ("60", 6, 0.3), ("0", 19, 0.3)])
+def test_heavy_read_pass_exact(fmi, monkeypatch, budget, min_seed, rep):
+    """Reads the lane kernel hands over after GB_FMI_HEAVY backwardExt calls are redone by the
+    wave-cooperative smem_heavy (one wave per read, 64 prev-list extensions per backward step): with
+    small budgets most reads take that path -- including reads promoted to big slots before the
+    hand-over (min_seed_len 6) and reads longer than 64 bases' lists -- and the SMEM lists, per-batch
+    and per-phase counts and backwardExt calls stay those of the oracle. Budget 0 = never hand over."""
     monkeypatch.setenv("GB_FMI_HEAVY", budget)
-    monkeypatch.setenv("GB_FMI_LIST", lst)
     ref = gen.fmi_reference(400_000, seed=51, repeat_frac=rep)
     codes, lens = gen.fmi_reads(ref, 2500, read_len=151, seed=52, sub_rate=0.03, n_rate=0.002)
     lens = lens.copy()
