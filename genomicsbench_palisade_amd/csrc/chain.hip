@@ -444,10 +444,9 @@ int validate(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, con
   return GB_OK;
 }
 
-// Uploads a validated call set into B, growing B's buffers only when they are too small. sync_end
-// false: x / y must stay valid until the batch's stream has passed the upload.
+// Uploads a validated call set into B, growing B's buffers only when they are too small.
 int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const float *avg_qspan,
-               const int32_t *params4, const uint64_t *x, const uint64_t *y, bool sync_end = true) {
+               const int32_t *params4, const uint64_t *x, const uint64_t *y) {
   if (int st = validate(ncalls, offsets, avg_qspan, params4, x, y)) return st;
   const int64_t na = offsets[ncalls];
   GB_HIP(hipSetDevice(B->device));
@@ -489,7 +488,7 @@ int batch_fill(gb_chain_batch *B, int64_t ncalls, const int64_t *offsets, const 
   }
   // the block table: whole calls, or long calls as speculative segments (chain_split.hip)
   const int st = gbchain::split_plan(B, offsets, x, params4);
-  if (sync_end) GB_HIP(hipStreamSynchronize(B->stream));  // the caller may free x / y on return
+  GB_HIP(hipStreamSynchronize(B->stream));  // the caller may free x / y on return
   return st;
 }
 
@@ -687,39 +686,24 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
   return GB_OK;
 }
 
-}  // extern "C"
-
-namespace {
-// Batch `slot` of this (host thread, device): kept for reuse by repeated one-shot calls (their
-// stream, events and grow-only buffers). Never freed (freeing at thread exit could run after the HIP
-// runtime is torn down).
-int cached_batch(int slot, gb_chain_batch **out) {
-  thread_local std::vector<std::pair<int, gb_chain_batch *>> ws;
-  int dev = 0;
-  GB_HIP(hipGetDevice(&dev));
-  const int key = dev * 4 + slot;
-  for (auto &w : ws)
-    if (w.first == key) {
-      *out = w.second;
-      return GB_OK;
-    }
-  gb_chain_batch *B = nullptr;
-  if (int st = batch_new(&B)) return st;
-  ws.emplace_back(key, B);
-  *out = B;
-  return GB_OK;
-}
-}  // namespace
-
-extern "C" {
-
 int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
              const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents, int32_t *targets,
              int32_t *peak_scores) {
+  // one cached batch per (host thread, device): repeated host_chain_kernel calls reuse its stream,
+  // events and grow-only buffers. Never freed (freeing at thread exit could run after the HIP
+  // runtime is torn down).
   int st = validate(ncalls, offsets, avg_qspan, params4, x, y);
   if (st) return st;
+  thread_local std::vector<std::pair<int, gb_chain_batch *>> ws;
+  int dev = 0;
+  GB_HIP(hipGetDevice(&dev));
   gb_chain_batch *B = nullptr;
-  if ((st = cached_batch(0, &B))) return st;
+  for (auto &w : ws)
+    if (w.first == dev) B = w.second;
+  if (!B) {
+    if ((st = batch_new(&B))) return st;
+    ws.emplace_back(dev, B);
+  }
   const bool hp = getenv("GB_CHAIN_HOSTPROF") != nullptr;
   const auto t0 = std::chrono::steady_clock::now();
   if ((st = batch_fill(B, ncalls, offsets, avg_qspan, params4, x, y))) return st;
@@ -735,62 +719,6 @@ int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, con
             ms(t1, t2), ms(t2, t3));
   }
   return st;
-}
-
-int gb_chain_pipelined(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
-                       const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents, int32_t *targets,
-                       int32_t *peak_scores, int chunks, gb_chain_piece_fn prep, gb_chain_piece_fn ready, void *user) {
-  gb::Range range_("gb.chain.pipelined");
-  GB_ARG(ncalls >= 0 && offsets, "gb_chain_pipelined: bad arguments");
-  const int64_t na = offsets[ncalls];
-  if (chunks <= 1 || ncalls < 2 * (int64_t)chunks) {
-    if (prep) prep(0, ncalls, user);
-    int st = gb_chain(ncalls, offsets, avg_qspan, params4, x, y, scores, parents, targets, peak_scores);
-    if (!st && ready) ready(0, ncalls, user);
-    return st;
-  }
-  // pieces [cut[k], cut[k+1]) balanced by anchors
-  std::vector<int64_t> cut((size_t)chunks + 1, ncalls);
-  cut[0] = 0;
-  for (int k = 1; k < chunks; k++)
-    cut[(size_t)k] = std::max(cut[(size_t)k - 1],
-                              (int64_t)(std::upper_bound(offsets, offsets + ncalls + 1, na * k / chunks) - offsets - 1));
-  gb_chain_batch *Bs[2];
-  for (int s = 0; s < 2; s++)
-    if (int st = cached_batch(1 + s, &Bs[s])) return st;
-  std::vector<int64_t> sub[2];
-  int64_t pend[2][2] = {{-1, -1}, {-1, -1}};  // the piece each batch still runs
-  auto finish = [&](int s) -> int {
-    if (pend[s][0] < 0) return GB_OK;
-    GB_HIP(hipStreamSynchronize(Bs[s]->stream));
-    if (ready) ready(pend[s][0], pend[s][1], user);
-    pend[s][0] = -1;
-    return GB_OK;
-  };
-  for (int k = 0; k < chunks; k++) {
-    const int64_t lo = cut[(size_t)k], hi = cut[(size_t)k + 1];
-    if (lo == hi) continue;
-    const int s = k & 1;
-    if (prep) prep(lo, hi, user);
-    if (int st = finish(s)) return st;  // the piece before last on this batch
-    gb_chain_batch *B = Bs[s];
-    std::vector<int64_t> &so = sub[s];
-    so.resize((size_t)(hi - lo) + 1);
-    for (int64_t c = lo; c <= hi; c++) so[(size_t)(c - lo)] = offsets[c] - offsets[lo];
-    const int64_t a0 = offsets[lo], n = offsets[hi] - a0;
-    if (int st = batch_fill(B, hi - lo, so.data(), avg_qspan + lo, params4 + 4 * lo, x + a0, y + a0, false)) return st;
-    if (int st = gb_chain_batch_run(B)) return st;
-    const size_t nn = (size_t)std::max<int64_t>(B->nanchors, 1);
-    int32_t *dst[4] = {scores, parents, targets, peak_scores};
-    for (int q = 0; q < 4; q++)
-      if (dst[q] && n) GB_HIP(hipMemcpyAsync(dst[q] + a0, B->d_out + q * nn, (size_t)n * 4, hipMemcpyDeviceToHost, B->stream));
-    pend[s][0] = lo;
-    pend[s][1] = hi;
-    if (int st = finish(s ^ 1)) return st;  // the previous piece, while this one runs
-  }
-  for (int s = 0; s < 2; s++)
-    if (int st = finish(s)) return st;
-  return GB_OK;
 }
 
 }  // extern "C"

@@ -1,10 +1,9 @@
 // chain_dropin.cpp -- host_chain_kernel (tools/minimap2-acceleration/kernel/scalar/src/host_kernel.cpp,
 // benchmarks/chain/src/host_kernel.cpp:481-501) over the C ABI of csrc/chain.hip.
-// The calls are flattened to CSR and run on the device, and the return vectors are resized and
+// The calls are flattened to CSR, run as one device batch, and the return vectors are resized and
 // filled like the reference's (ret[c].n = n, four vectors of n entries). The flatten and the fill
 // are spread over host threads (calls balanced by anchors), into and out of page-locked staging
-// buffers kept per calling thread, so the H2D / D2H copies run at DMA rate; big batches go in
-// pieces whose flatten, copies, kernels and fill overlap (gb_chain_pipelined).
+// buffers kept per calling thread, so the H2D / D2H copies run at DMA rate.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -56,8 +55,7 @@ struct Pinned {
   }
 };
 
-// run f(lo, hi) over [0, ncalls) in up to `nt` contiguous pieces balanced by anchors (off: the
-// calls' anchor offsets, off[0] not necessarily 0)
+// run f(lo, hi) over [0, ncalls) in up to `nt` contiguous pieces balanced by anchors
 template <typename F>
 void parallel_calls(int64_t ncalls, const int64_t *off, int nt, F f) {
   if (nt <= 1 || ncalls < 2) {
@@ -67,7 +65,7 @@ void parallel_calls(int64_t ncalls, const int64_t *off, int nt, F f) {
   std::vector<int64_t> cut((size_t)nt + 1, ncalls);
   cut[0] = 0;
   for (int t = 1; t < nt; t++)
-    cut[(size_t)t] = std::upper_bound(off, off + ncalls + 1, off[0] + (off[ncalls] - off[0]) * t / nt) - off - 1;
+    cut[(size_t)t] = std::upper_bound(off, off + ncalls + 1, off[ncalls] * t / nt) - off - 1;
   for (int t = 1; t <= nt; t++) cut[(size_t)t] = std::max(cut[(size_t)t], cut[(size_t)t - 1]);
   std::vector<std::thread> th;
   for (int t = 1; t < nt; t++) th.emplace_back(f, cut[(size_t)t], cut[(size_t)t + 1]);
@@ -91,65 +89,42 @@ void host_chain_kernel(std::vector<call_t> &arg, std::vector<return_t> &ret, int
   int32_t *out = bout.get<int32_t>(4 * (size_t)std::max<int64_t>(na, 1));
   std::vector<float> aq((size_t)nc);
   std::vector<int32_t> p4((size_t)nc * 4);
+  parallel_calls(nc, off.data(), nt, [&](int64_t lo, int64_t hi) {
+    for (int64_t c = lo; c < hi; c++) {
+      const call_t &a = arg[c];
+      const anchor_t *an = a.anchors.data();
+      for (size_t k = 0; k < a.anchors.size(); k++) {
+        x[off[c] + k] = an[k].x;
+        y[off[c] + k] = an[k].y;
+      }
+      aq[c] = a.avg_qspan;
+      p4[4 * c] = a.max_dist_x;
+      p4[4 * c + 1] = a.max_dist_y;
+      p4[4 * c + 2] = a.bw;
+      p4[4 * c + 3] = a.n_segs;
+    }
+  });
   const size_t nn = (size_t)std::max<int64_t>(na, 1);
   int32_t *sc = out, *par = out + nn, *tg = out + 2 * nn, *pk = out + 3 * nn;
+  const auto t1 = std::chrono::steady_clock::now();
+  int st = gb_chain(nc, off.data(), aq.data(), p4.data(), x, y, sc, par, tg, pk);
+  const auto t2 = std::chrono::steady_clock::now();
+  if (st) die("gb_chain", st);
   ret.resize((size_t)nc);
-  // The calls go through in pieces (GB_CHAIN_CHUNKS, default 4 for batches of a million anchors or
-  // more): a piece is flattened while the one before it runs on the GPU, and its return vectors are
-  // filled while the next one runs (gb_chain_pipelined).
-  struct Ctx {
-    std::vector<call_t> *arg;
-    std::vector<return_t> *ret;
-    const int64_t *off;
-    int nt;
-    uint64_t *x, *y;
-    float *aq;
-    int32_t *p4, *sc, *par, *tg, *pk;
-    double prep_ms, ready_ms;
-  } cx{&arg, &ret, off.data(), nt, x, y, aq.data(), p4.data(), sc, par, tg, pk, 0, 0};
-  auto prep = [](int64_t lo, int64_t hi, void *u) {
-    Ctx &C = *static_cast<Ctx *>(u);
-    const auto a = std::chrono::steady_clock::now();
-    parallel_calls(hi - lo, C.off + lo, C.nt, [&](int64_t l, int64_t h) {
-      for (int64_t c = lo + l; c < lo + h; c++) {
-        const call_t &k = (*C.arg)[c];
-        const anchor_t *an = k.anchors.data();
-        for (size_t j = 0; j < k.anchors.size(); j++) {
-          C.x[C.off[c] + j] = an[j].x;
-          C.y[C.off[c] + j] = an[j].y;
-        }
-        C.aq[c] = k.avg_qspan;
-        C.p4[4 * c] = k.max_dist_x;
-        C.p4[4 * c + 1] = k.max_dist_y;
-        C.p4[4 * c + 2] = k.bw;
-        C.p4[4 * c + 3] = k.n_segs;
-      }
-    });
-    C.prep_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-  };
-  auto ready = [](int64_t lo, int64_t hi, void *u) {
-    Ctx &C = *static_cast<Ctx *>(u);
-    const auto a = std::chrono::steady_clock::now();
-    parallel_calls(hi - lo, C.off + lo, C.nt, [&](int64_t l, int64_t h) {
-      for (int64_t c = lo + l; c < lo + h; c++) {
-        return_t &r = (*C.ret)[c];
-        const int64_t s = C.off[c], e = C.off[c + 1];
-        r.n = e - s;
-        r.scores.assign(C.sc + s, C.sc + e);
-        r.parents.assign(C.par + s, C.par + e);
-        r.targets.assign(C.tg + s, C.tg + e);
-        r.peak_scores.assign(C.pk + s, C.pk + e);
-      }
-    });
-    C.ready_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-  };
-  const char *ce = getenv("GB_CHAIN_CHUNKS");
-  const int chunks = ce ? atoi(ce) : (na >= 1000000 ? 4 : 1);
-  const int st = gb_chain_pipelined(nc, off.data(), aq.data(), p4.data(), x, y, sc, par, tg, pk, chunks, prep, ready, &cx);
-  if (st) die("gb_chain_pipelined", st);
+  parallel_calls(nc, off.data(), nt, [&](int64_t lo, int64_t hi) {
+    for (int64_t c = lo; c < hi; c++) {
+      return_t &r = ret[c];
+      const int64_t a = off[c], b = off[c + 1];
+      r.n = b - a;
+      r.scores.assign(sc + a, sc + b);
+      r.parents.assign(par + a, par + b);
+      r.targets.assign(tg + a, tg + b);
+      r.peak_scores.assign(pk + a, pk + b);
+    }
+  });
   if (getenv("GB_CHAIN_HOSTPROF")) {
-    const double all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    fprintf(stderr, "[host_chain_kernel] %d piece(s): %.2f ms, of which flatten %.2f ms, return vectors %.2f ms (%d threads)\n",
-            chunks, all, cx.prep_ms, cx.ready_ms, nt);
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[host_chain_kernel] flatten %.2f ms, gb_chain %.2f ms, return vectors %.2f ms (%d threads)\n",
+            ms(t0, t1), ms(t1, t2), ms(t2, std::chrono::steady_clock::now()), nt);
   }
 }

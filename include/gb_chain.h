@@ -64,18 +64,6 @@ int gb_chain(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, con
              const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents,
              int32_t *targets, int32_t *peak_scores);
 
-/* Pipelined one-shot form (host_chain_kernel's: the calls' inputs and outputs live in host memory,
- * ideally page-locked, gb_host_alloc). The calls are cut into `chunks` pieces balanced by anchors;
- * piece k's upload, kernels and download overlap the other pieces' on two batches. prep(lo, hi, user)
- * is called before calls [lo, hi) are uploaded (the caller may fill x / y / avg_qspan / params4 of
- * exactly those calls there, while earlier pieces run), ready(lo, hi, user) once their four outputs
- * are in place (while later pieces run); both on the calling thread, in call order, and may be NULL.
- * chunks <= 1 is gb_chain with the two callbacks around it. */
-typedef void (*gb_chain_piece_fn)(int64_t lo, int64_t hi, void *user);
-int gb_chain_pipelined(int64_t ncalls, const int64_t *offsets, const float *avg_qspan, const int32_t *params4,
-                       const uint64_t *x, const uint64_t *y, int32_t *scores, int32_t *parents, int32_t *targets,
-                       int32_t *peak_scores, int chunks, gb_chain_piece_fn prep, gb_chain_piece_fn ready, void *user);
-
 #ifdef __cplusplus
 }
 #endif

@@ -193,32 +193,3 @@ def test_gpu_split_remark_wide_windows(monkeypatch, split, fault):
     ns, rounds, fixups = b.split_stats()
     assert ns == calls.ncalls and fixups >= ns and rounds > 1
     b.close()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("chunks,split", [("1", ""), ("3", ""), ("7", "256,0"), ("2", "0")])
-def test_gpu_host_chain_kernel_pieces(split_calls, golden, monkeypatch, chunks, split):
-    """host_chain_kernel over std::vector<call_t> (tests/cpp/dropin_bench.cpp, as main.cpp:80-91 calls
-    it) in GB_CHAIN_CHUNKS pieces whose flatten, copies, kernels and return vectors overlap
-    (gb_chain_pipelined): every output equals the reference loop's, with split calls spanning piece
-    boundaries or not."""
-    import ctypes
-    from conftest import ROOT
-    from genomicsbench_palisade_amd import set_device
-    set_device(0)
-    monkeypatch.setenv("GB_CHAIN_CHUNKS", chunks)
-    monkeypatch.setenv("GB_CHAIN_SPLIT", split)
-    lib = ctypes.CDLL(os.path.join(ROOT, "tests", "_build", "libdropin_bench.so"))
-    vp = ctypes.c_void_p
-    lib.bench_host_chain_kernel.argtypes = [ctypes.c_int64, vp, vp, vp, vp, vp, ctypes.c_int, vp, vp, vp, vp]
-    lib.bench_host_chain_kernel.restype = ctypes.c_double
-    calls, exp = split_calls
-    calls = _concat_calls([golden[0], calls, golden[0]])
-    exp = tuple(np.concatenate([g, e, g]) for g, e in zip(golden[1], exp))
-    n = calls.nanchors
-    out = [np.zeros(n, np.int32) for _ in range(4)]
-    t = lib.bench_host_chain_kernel(calls.ncalls, calls.offsets.ctypes.data, calls.avg_qspan.ctypes.data,
-                                    calls.params4.ctypes.data, calls.x.ctypes.data, calls.y.ctypes.data, 8,
-                                    *[o.ctypes.data for o in out])
-    assert t > 0
-    assert_same(tuple(out), exp)
