@@ -718,6 +718,33 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
            s.len1, s.len2, GB_BSW_MAX_QLEN);
     GB_ARG(false, "gb_bsw_batch_create: pair %lld lies outside the sequence buffers", (long long)p);
   }
+  // Tail balance for batches that fill the chip only about once with lane waves: then the step is
+  // the slowest lane wave, a wave of the longest pairs of the widest variants (~rows x chunks x
+  // 0.28 us: ~1.4 ms for 250 rows at NCH 20), while the wave-per-pair kernel takes such a pair in
+  // tens of microseconds. The fraction GB_BSW_TAIL (default 0.1) of the lane pairs with the
+  // largest rows x chunks moves to the wave-per-pair kernel, which runs beside the lane kernels.
+  {
+    const char *te = getenv("GB_BSW_TAIL");
+    const double frac = te ? atof(te) : 0.1;  // r03ab, 100 k pairs: 0 228, 0.05 234, 0.1 258, 0.2 243 GCUPS
+    const int64_t fill = (int64_t)64 * 8 * std::max(B->num_cus, 1);  // lane waves of 64 pairs, 2 per SIMD
+    if (frac > 0 && n >= 1024 && n <= 2 * fill) {
+      std::vector<uint32_t> cost;
+      cost.reserve((size_t)n);
+      for (int64_t p = 0; p < n; ++p)
+        if (var[p] < 5) cost.push_back((uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)));
+      const size_t k = (size_t)((double)cost.size() * frac);
+      if (k > 0 && k < cost.size()) {
+        std::nth_element(cost.begin(), cost.end() - (ptrdiff_t)k, cost.end());
+        const uint32_t cut = *(cost.end() - (ptrdiff_t)k);
+        for (int64_t p = 0; p < n; ++p)
+          if (var[p] < 5 && (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)) >= cut) {
+            var[p] = 5;
+            keys[p] = (uint32_t)(((size_t)5 * kQB + (size_t)(kQB - 1 - std::min(P[p].qlen >> 2, kQB - 1))) * kTB +
+                                 (size_t)(kTB - 1 - std::min(P[p].tlen, kTB - 1)));
+          }
+      }
+    }
+  }
   std::vector<uint32_t> order((size_t)n);
   if (n < (1 << 16)) {
     // small batches: a stable comparison sort (the counting sort's 1.3 M-entry histogram would cost
