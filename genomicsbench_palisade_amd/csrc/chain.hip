@@ -516,20 +516,31 @@ int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool s
   A.prof = prof ? B->d_prof : nullptr;
   A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
   const dim3 g((unsigned)nvc), b(128);
+  static bool attr = false;
+  if (!attr) {
+    for (const void *f : {(const void *)chain_kernel<0, kRingSmall>, (const void *)chain_kernel<1, kRingSmall>,
+                          (const void *)chain_kernel<2, kRingSmall>, (const void *)chain_kernel<0, kRing>,
+                          (const void *)chain_kernel<1, kRing>, (const void *)chain_kernel<2, kRing>})
+      GB_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    attr = true;
+  }
+  const size_t lds_small = sizeof(uint32_t) * (kRingSmall + 64) + sizeof(Slot) * kSlots + 16;
+  const size_t lds_full = sizeof(uint32_t) * (kRing + 64) + sizeof(Slot) * kSlots + 16;
+  const size_t dyn = spread_lds(nvc, 2, small ? lds_small : lds_full);
   if (small) {
     if (prof == 2)
-      hipLaunchKernelGGL((chain_kernel<2, kRingSmall>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<2, kRingSmall>), g, b, dyn, stream, A);
     else if (prof == 1)
-      hipLaunchKernelGGL((chain_kernel<1, kRingSmall>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<1, kRingSmall>), g, b, dyn, stream, A);
     else
-      hipLaunchKernelGGL((chain_kernel<0, kRingSmall>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<0, kRingSmall>), g, b, dyn, stream, A);
   } else {
     if (prof == 2)
-      hipLaunchKernelGGL((chain_kernel<2, kRing>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<2, kRing>), g, b, dyn, stream, A);
     else if (prof == 1)
-      hipLaunchKernelGGL((chain_kernel<1, kRing>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<1, kRing>), g, b, dyn, stream, A);
     else
-      hipLaunchKernelGGL((chain_kernel<0, kRing>), g, b, 0, stream, A);
+      hipLaunchKernelGGL((chain_kernel<0, kRing>), g, b, dyn, stream, A);
   }
   GB_HIP(hipGetLastError());
   return GB_OK;
@@ -538,6 +549,23 @@ int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool s
 // The block table of a batch: small-ring blocks first (on the batch's stream), full-ring blocks
 // concurrently on the second stream.
 int launch_table(gb_chain_batch *B, int prof) {
+  if (B->n_rows > 0) {
+    // chain_rows blocks on the batch stream (their targets / scratch marks cleared first), the
+    // rest (unsorted calls: rare) on the second stream beside them
+    const int nr = B->n_rows, nvc = (int)B->vc.size(), ns = B->n_small;
+    GB_HIP(hipMemsetAsync(B->d_out + 2 * std::max<int64_t>(B->nanchors, 1), 0, (size_t)B->nanchors * 4, B->stream));
+    if (B->scratch_n > 0) GB_HIP(hipMemsetAsync(B->d_smark, 0, (size_t)B->scratch_n * 4, B->stream));
+    if (nr < nvc) {
+      GB_HIP(hipEventRecord(B->fj[0], B->stream));
+      GB_HIP(hipStreamWaitEvent(B->stream2, B->fj[0], 0));
+      if (int st = launch_chain(B, B->d_vc + nr, ns, prof, true, B->stream2)) return st;
+      if (int st = launch_chain(B, B->d_vc + nr + ns, nvc - nr - ns, prof, false, B->stream2)) return st;
+      GB_HIP(hipEventRecord(B->fj[1], B->stream2));
+    }
+    if (int st = launch_rows(B, B->d_vc, nr, B->stream)) return st;
+    if (nr < nvc) GB_HIP(hipStreamWaitEvent(B->stream, B->fj[1], 0));
+    return GB_OK;
+  }
   const int nvc = (int)B->vc.size(), ns = B->n_small;
   if (ns < nvc && ns > 0) {
     GB_HIP(hipEventRecord(B->fj[0], B->stream));

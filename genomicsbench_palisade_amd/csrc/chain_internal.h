@@ -59,9 +59,10 @@ struct gb_chain_batch {
   bool ran = false;
   gbchain::ChainBt *bt = nullptr;  // backtrack state (gb_chain_batch_backtrack)
 
-  // the block table of the sequential kernel: n_small small-ring blocks, then the others, each
-  // class longest first
+  // the block table: n_rows blocks for chain_rows (sorted x, chain_rows.hip), then n_small
+  // small-ring blocks and the full-ring ones for chain_kernel, each class longest first
   std::vector<gbchain::VCall> vc;
+  int n_rows = 0;
   int n_small = 0;
   gbchain::VCall *d_vc = nullptr;
   int64_t cap_vc = 0;
@@ -77,13 +78,14 @@ struct gb_chain_batch {
   gbchain::Chunk *d_chunks = nullptr;
   int32_t *d_st = nullptr;        // st, chunk-space index
   int32_t *d_sscore = nullptr, *d_sparent = nullptr;  // segment scratch
+  int32_t *d_smark = nullptr;     // segment scratch: targets marks of chain_rows' speculative blocks
   int32_t *d_front = nullptr;     // per split call: first anchor not known to be final
   int32_t *d_fail = nullptr;      // per split call: first anchor whose guess failed verification
   int32_t *d_link[2] = {nullptr, nullptr};  // pointer jumping (chunk-space index or -1)
   int32_t *d_val[2] = {nullptr, nullptr};
   int32_t *d_t2 = nullptr;                 // split anchors' targets marks, merged at the end
   unsigned long long *d_viscall = nullptr; // visited pairs per split call
-  int64_t cap_split = 0, cap_segs = 0, cap_chunks = 0, cap_st = 0, cap_sscore = 0, cap_sparent = 0, cap_front = 0,
+  int64_t cap_split = 0, cap_segs = 0, cap_chunks = 0, cap_st = 0, cap_sscore = 0, cap_sparent = 0, cap_smark = 0, cap_front = 0,
           cap_jump = 0, cap_t2 = 0, cap_viscall = 0;
   int64_t spec_rounds = 0, fixups = 0;  // statistics of the last run
 };
@@ -95,4 +97,10 @@ int split_resolve(gb_chain_batch *B);
 void split_free(gb_chain_batch *B);
 int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool small, hipStream_t stream);
 int launch_table(gb_chain_batch *B, int prof);
+// chain_rows.hip
+int launch_rows(gb_chain_batch *B, const VCall *d_vc, int nvc, hipStream_t stream);
+// Dynamic LDS that spreads a launch of nwg workgroups (waves_per_wg waves each, static_lds bytes of
+// LDS each) over every SIMD: a launch with fewer waves than SIMD slots is latency-bound, and the
+// dispatcher otherwise stacks its workgroups on few CUs. 0 when the launch fills the chip anyway.
+size_t spread_lds(int nwg, int waves_per_wg, size_t static_lds);
 }  // namespace gbchain

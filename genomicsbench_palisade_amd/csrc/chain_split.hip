@@ -42,8 +42,8 @@
 
 namespace gbchain {
 
-constexpr int kSegDefault = 4096;   // segment length
-constexpr int kWarmDefault = 256;   // warm-up anchors before the window of a segment's first anchor
+constexpr int kSegDefault = 4096;   // longest segment
+constexpr int kWarmDefault = 128;   // warm-up anchors before the window of a segment's first anchor
 constexpr int kFix = 1024;          // anchors recomputed sequentially after a failed guess
 constexpr int kTagRing = 1024;      // verification stamp ring (tagged, see resolve_tagged)
 
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(64) void guess_init(SplitArgs A, int32_t *link, int
     val[j] = 0;
     return;
   }
-  const int32_t s = min(i / S.c1, S.nseg - 1);  // segments are c1 anchors long, the last one longer
+  const int32_t s = min(i / S.c1, S.nseg - 1);  // segments are c1 anchors long, the last one shorter
   const Seg G = A.segs[S.seg0 + s];
   const int32_t fs = A.s_score[G.soff + (i - G.as)], q = A.s_parent[G.soff + (i - G.as)];
   const int32_t p = q >= 0 ? q + G.as : -1;
@@ -312,15 +312,16 @@ int grow(T **p, int64_t *cap, int64_t need) {
   return GB_OK;
 }
 
-// Segment length: as long as the segment's sequential run stays well under the batch's throughput
-// time (~0.53 us per anchor of one block, ~0.26 ns per anchor of the whole batch at 16 blocks per
-// CU), so small batches get shorter segments: 'large' (25 M anchors) 4096, a 2.5 M-anchor batch
-// 1024 (measured: small set 505 -> 1149 Manchors/s, large set 2 913 at 4096 vs 1 648 at 1024).
-// GB_CHAIN_SPLIT: "0" runs every call whole; "SEG[,WARM]" sets the segment length and warm-up
+// Segment length: as long as the segment's sequential run (its window and warm-up included) stays
+// under the batch's throughput time, so small batches get shorter segments; shorter ones cost more
+// verification and warm-up work. GB_CHAIN_SPLIT: "0" runs every call whole; "SEG[,WARM]" sets the segment length and warm-up
 // (tests force tiny segments without warm-up to exercise the fix-up path).
 void split_knobs(int64_t total_anchors, int *seg, int *warm) {
+  // the power of two in [512, 4096] nearest below total / 12 000 (measured with chain_rows,
+  // tools/chain_rows_probe.py: 'large' 25.4 M anchors 2048 (7.76 ms; 4096 7.87, 1024 10.3), 'small'
+  // 2.5 M and the 1/8 shard 3.2 M anchors 512 (2.06 / 2.20 ms; 1024 2.29 / 2.38)
   *seg = kSegDefault;
-  while (*seg > 1024 && (int64_t)(*seg + 600) * 4077 > total_anchors) *seg /= 2;
+  while (*seg > 512 && (int64_t)*seg * 12000 > total_anchors) *seg /= 2;
   *warm = kWarmDefault;
   const char *e = getenv("GB_CHAIN_SPLIT");
   if (!e || !*e) return;
@@ -398,10 +399,16 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   // host_kernel.cpp:57-58) and whether x is sorted; calls in parallel
   std::vector<int32_t> maxwin((size_t)ncalls, 0);
   std::vector<uint8_t> sorted((size_t)ncalls, 0);
+  // chain_rows takes the blocks of calls whose window test is monotone in j: x sorted and
+  // x + max_dist_x without wrap-around (GB_CHAIN_ROWS=0: chain_kernel for every block)
+  std::vector<uint8_t> mono((size_t)ncalls, 0);
+  const char *rows_env = getenv("GB_CHAIN_ROWS");
+  const bool rows_on = !(rows_env && rows_env[0] == '0');
   // split candidates (>= 2 segments): st(i) kept, and per segment its warm-up start and widest
   // window, all computed in the parallel pass
   struct Cand {
     std::vector<int32_t> st, as, win;
+    int32_t L = 0;  // segment length: n split into ceil(n / seg) equal segments (the last one shorter)
   };
   std::vector<Cand> cand((size_t)ncalls);
   auto walk = [&](int64_t c, int32_t *stw) {
@@ -419,6 +426,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     }
     maxwin[(size_t)c] = mw;
     sorted[(size_t)c] = srt;
+    mono[(size_t)c] = srt && (int64_t)mdx >= 0 && (n == 0 || x[off + n - 1] + mdx >= x[off + n - 1]);
   };
   {
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
@@ -439,11 +447,14 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
             K.st = std::vector<int32_t>();
             continue;
           }
-          const int32_t nseg = n / seg;
+          // equal segments of at most seg anchors: the longest block of the launch (a segment, its
+          // window and its warm-up) is then bounded by seg, not by a last segment of up to 2 seg - 1
+          const int32_t nseg = (n + seg - 1) / seg, L = (n + nseg - 1) / nseg;
+          K.L = L;
           K.as.resize((size_t)nseg);
           K.win.resize((size_t)nseg);
           for (int32_t k = 0; k < nseg; k++) {
-            const int32_t cs = k * seg, es = k + 1 == nseg ? n : (k + 1) * seg;
+            const int32_t cs = k * L, es = k + 1 == nseg ? n : (k + 1) * L;
             const int32_t a = k == 0 ? 0 : std::max(0, K.st[(size_t)cs] - warm);
             int32_t w = 0;
             for (int32_t i = a; i < es; i++) w = std::max(w, i - std::max(a, K.st[(size_t)i]));
@@ -455,7 +466,8 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     for (auto &t : th) t.join();
   }
   auto vpush = [&](int64_t in, int64_t out, int32_t n, int64_t c, int32_t mode, int32_t win) {
-    B->vc.push_back({in, out, n, (int32_t)c, 0, mode, 0, win <= kRingSmall ? 1 : 0});
+    const int32_t cls = (rows_on && mono[(size_t)c]) ? 2 : (win <= kRingSmall ? 1 : 0);
+    B->vc.push_back({in, out, n, (int32_t)c, 0, mode, 0, cls});
   };
   for (int64_t c = 0; c < ncalls; c++) {
     const int64_t off = offsets[c];
@@ -473,15 +485,15 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     S.n = n;
     S.call = (int32_t)c;
     S.seg0 = (int32_t)B->segs.size();
-    S.nseg = n / seg;
-    S.c1 = seg;
+    S.nseg = (int32_t)K.as.size();
+    S.c1 = K.L;
     S.cbase = (int32_t)B->chunks.size();
-    vpush(off, off, seg, c, kVFinal, K.win[0]);  // segment 0: exact
-    B->segs.push_back({0, seg, 0, 0, -1});
+    vpush(off, off, K.L, c, kVFinal, K.win[0]);  // segment 0: exact
+    B->segs.push_back({0, K.L, 0, 0, -1});
     for (int32_t k = 1; k < S.nseg; k++) {
       Seg G;
-      G.cs = k * seg;
-      G.es = k + 1 == S.nseg ? n : (k + 1) * seg;
+      G.cs = k * K.L;
+      G.es = k + 1 == S.nseg ? n : (k + 1) * K.L;
       G.as = K.as[(size_t)k];
       G.pad = 0;
       G.soff = B->scratch_n;
@@ -496,14 +508,17 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
     B->split.push_back(S);
     B->max_split_n = std::max(B->max_split_n, n);
   }
-  // small-ring blocks, then the others (VCall::pad holds the class until here); longest first in
-  // each: the grid is dispatched in order, so the critical paths start first
+  // chain_rows blocks, small-ring blocks, then the others (VCall::pad holds the class until here);
+  // longest first in each: the grid is dispatched in order, so the critical paths start first (and
+  // the two halves of a chain_rows wave get blocks of about the same length)
   std::stable_sort(B->vc.begin(), B->vc.end(), [](const VCall &a, const VCall &b) {
     return a.pad != b.pad ? a.pad > b.pad : a.n > b.n;
   });
+  B->n_rows = 0;
   B->n_small = 0;
   for (auto &v : B->vc) {
-    B->n_small += v.pad;
+    B->n_rows += v.pad == 2;
+    B->n_small += v.pad == 1;
     v.pad = 0;
   }
   const int64_t nvc = (int64_t)B->vc.size();
@@ -518,6 +533,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   if (!st) st = grow(&B->d_st, &B->cap_st, 64 * nch);
   if (!st) st = grow(&B->d_sscore, &B->cap_sscore, B->scratch_n);
   if (!st) st = grow(&B->d_sparent, &B->cap_sparent, B->scratch_n);
+  if (!st) st = grow(&B->d_smark, &B->cap_smark, B->scratch_n);
   if (!st) st = grow(&B->d_front, &B->cap_front, 2 * ns);
   if (!st) st = grow(&B->d_viscall, &B->cap_viscall, ns);
   if (!st) st = grow(&B->d_t2, &B->cap_t2, B->nanchors);
@@ -622,7 +638,7 @@ void split_free(gb_chain_batch *B) {
   for (void *p : {(void *)B->d_vc, (void *)B->d_split, (void *)B->d_segs, (void *)B->d_chunks, (void *)B->d_st,
                   (void *)B->d_sscore, (void *)B->d_sparent, (void *)B->d_front, (void *)B->d_link[0],
                   (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1], (void *)B->d_t2,
-                  (void *)B->d_viscall})
+                  (void *)B->d_viscall, (void *)B->d_smark})
     (void)hipFree(p);
   B->d_vc = nullptr;
 }

@@ -56,10 +56,13 @@ def test_gpu_vs_golden(golden):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows", ["1", "0"])
 @pytest.mark.parametrize("seed,ncalls,median,maxn", [(1, 300, 1500, 87271), (2, 2000, 200, 5000)])
-def test_gpu_vs_oracle(seed, ncalls, median, maxn):
+def test_gpu_vs_oracle(seed, ncalls, median, maxn, rows, monkeypatch):
+    """rows "1": sorted calls on chain_rows (two calls per wave), "0": chain_kernel for every block."""
     from genomicsbench_palisade_amd import chain, set_device
     set_device(0)
+    monkeypatch.setenv("GB_CHAIN_ROWS", rows)
     calls = gen.chain_dataset("small", num_calls=ncalls, seed=seed, median_n=median, max_n=maxn)
     exp = oracle_lib.chain_oracle(calls, 8)
     b = chain.ChainBatch(calls)
@@ -138,8 +141,9 @@ def split_calls():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("split,fault", [("", 0), ("0", 0), ("256,0", 0), ("64,0", 0), ("128,8", 37), ("", 997)])
-def test_gpu_split_exact(split_calls, monkeypatch, split, fault):
+@pytest.mark.parametrize("split,fault,rows", [("", 0, "1"), ("0", 0, "1"), ("256,0", 0, "1"), ("64,0", 0, "1"),
+                                              ("128,8", 37, "1"), ("", 997, "1"), ("", 0, "0"), ("128,8", 37, "0")])
+def test_gpu_split_exact(split_calls, monkeypatch, split, fault, rows):
     """Long calls as speculative segments (csrc/chain_split.hip) give the sequential loop's results
     bit for bit: default and tiny segments, no warm-up, and injected wrong guesses that the
     verification must catch and the sequential fix-up repair."""
@@ -148,6 +152,7 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault):
     calls, exp = split_calls
     monkeypatch.setenv("GB_CHAIN_SPLIT", split)
     monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
+    monkeypatch.setenv("GB_CHAIN_ROWS", rows)
     b = chain.ChainBatch(calls)
     b.run()
     got = b.results()
@@ -157,8 +162,8 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault):
     if split == "0":
         assert ns == 0
     else:
-        # default: the segment length adapts to the batch (1024..4096 anchors, chain_split.hip)
-        seg = int(split.split(",")[0]) if split else 1024
+        # default: the segment length adapts to the batch (512..4096 anchors, chain_split.hip)
+        seg = int(split.split(",")[0]) if split else 512
         long_calls = sum(1 for c in range(calls.ncalls) if calls.offsets[c + 1] - calls.offsets[c] >= 2 * seg)
         assert 0 < ns < long_calls  # the unsorted long call stays whole
     if fault:
@@ -192,4 +197,38 @@ def test_gpu_split_remark_wide_windows(monkeypatch, split, fault):
     assert got[4] == exp[4]
     ns, rounds, fixups = b.split_stats()
     assert ns == calls.ncalls and fixups >= ns and rounds > 1
+    b.close()
+
+
+def _long_window_call(rng, n, frac_chain):
+    """x step 1, so every window holds max_iter (5 000) anchors; most anchors have dq <= 0 against
+    their predecessors (filtered, no parents, no marks), so loops rarely break and visit far more than
+    64 candidates: chain_rows' HBM path (candidates older than its 64-anchor ring, global marks)."""
+    x = (np.arange(n) + 1000).astype(np.uint64)
+    y = rng.integers(0, 1 << 20, n).astype(np.int64)
+    on = rng.random(n) < frac_chain
+    y[on] = x[on].astype(np.int64) + rng.integers(-3, 4, int(on.sum()))
+    yy = (np.uint64(15) << np.uint64(32)) | y.astype(np.uint64)
+    return gen.ChainCalls(np.array([0, n]), x, yy, np.array([15.0], np.float32),
+                          np.array([[5000, 5000, 500, 1]], np.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", ["0", "1024,64"])
+def test_gpu_rows_long_windows(monkeypatch, split):
+    """chain_rows past its ring: visited counts far above 64, marks from HBM, whole and split calls."""
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    rng = np.random.default_rng(5)
+    calls = _concat_calls([_long_window_call(rng, 9000, 0.05), _long_window_call(rng, 7000, 0.3),
+                           _long_window_call(rng, 3000, 0.8), _cloud_call(rng, 6000, 40, 4000, (0, 1), 200)])
+    exp = oracle_lib.chain_oracle(calls, 8)
+    assert exp[4] > 64 * calls.nanchors // 4  # the HBM path is exercised
+    monkeypatch.setenv("GB_CHAIN_SPLIT", split)
+    monkeypatch.setenv("GB_CHAIN_ROWS", "1")
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
     b.close()
