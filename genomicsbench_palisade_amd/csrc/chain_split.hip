@@ -204,10 +204,13 @@ __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, 
 // mark overwrite its own earlier one (a clash), which fails the anchor. The re-mark pass (whose
 // marks and visited counts are final) uses an 8 K ring, wider than any window (max_iter 5000 + 64
 // lanes), so no mark is ever lost there.
+// need (from verify_lanes): only the anchors whose bit is set (null: all of them).
 template <bool CHECK, int RING = CHECK ? kTagRing : 8192>
-__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
+__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const uint64_t *need) {
   static_assert(CHECK || RING > kMaxIter + 64, "the re-mark ring must hold any window");
   __shared__ uint32_t S[RING + 64];
+  const uint64_t nd = need ? need[blockIdx.x] : ~0ull;
+  if (!nd) return;
   const Chunk ch = A.chunks[blockIdx.x];
   const SplitCall Sc = A.split[ch.sc];
   const int lane = threadIdx.x;
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
     const int32_t i = start + k;
     const uint64_t xi = rfl64_lane(bx, k), yi = rfl64_lane(by, k);
     const int32_t fi = __builtin_amdgcn_readlane(bf, k), pi = __builtin_amdgcn_readlane(bp, k);
-    if (i >= front) {
+    if (i >= front && ((nd >> k) & 1)) {
       const int32_t st = __builtin_amdgcn_readlane(bst, k);
       int32_t sg;
       const bool ok = geometry(xi, yi, wx, wy, i - 1 - lane >= st, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
@@ -278,6 +281,117 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A) {
   if (lane == 0) {
     if (CHECK && first_bad != INT_MAX) atomicMin(A.fail + ch.sc, first_bad);
     atomicAdd(A.viscall + ch.sc, (unsigned long long)vis);
+  }
+}
+
+// 2'. verify, one anchor per lane (the common case, ahead of verify_kernel): lane l re-runs the
+// reference loop of anchor start + l over its first 64 candidates, reading the guessed window from
+// memory (neighbouring lanes read neighbouring anchors), with the "targets[j] == i" marks of its own
+// loop as bits of a 64-bit mask (bit d: position i-1-d; a mark further back matters only to a loop
+// that visits more than 64 candidates). Such loops -- no break and a window wider than 64 -- are
+// left to verify_kernel through need[chunk]; every other anchor is decided here, with the same
+// outputs (fail, t2 marks, visited pairs). About one wave instruction per lane-candidate instead of
+// a 64-lane step per candidate block of every anchor.
+template <bool CHECK>
+__global__ __launch_bounds__(64) void verify_lanes(SplitArgs A, uint64_t *need) {
+  // targets marks of the wave's 64 loops, max-reduced in LDS over positions [start - 192, start + 64)
+  // before they go to t2 (neighbouring anchors visit the same candidates: one global atomic per
+  // position instead of one per visited candidate, which made the pass atomic-bound)
+  constexpr int kMarkLo = 192, kMarkN = 256;
+  __shared__ int32_t lm[kMarkN];
+  const Chunk ch = A.chunks[blockIdx.x];
+  const SplitCall Sc = A.split[ch.sc];
+  const int lane = threadIdx.x;
+  const int32_t start = ch.start, n = Sc.n;
+  const int32_t front = A.front[ch.sc];
+  const int32_t i = start + lane;
+  const bool mine = (i < n) & (i >= front);
+  if (!__builtin_amdgcn_ballot_w64(mine)) {
+    if (lane == 0) need[blockIdx.x] = 0;
+    return;
+  }
+  const int c = Sc.call;
+  const int max_dist_x = A.params4[4 * c], max_dist_y = A.params4[4 * c + 1];
+  const int bw = A.params4[4 * c + 2], n_segs = A.params4[4 * c + 3];
+  const double avg_qspan = (double)A.avg_qspan[c];
+  const uint64_t *X = A.x + Sc.off, *Y = A.y + Sc.off;
+  const int32_t *score = A.score + Sc.off, *parent = A.parent + Sc.off;
+  int32_t *tgt = A.t2 + Sc.off;
+  const int32_t ii = min(i, n - 1);
+  const uint64_t xi = X[ii], yi = Y[ii];
+  const int32_t fi = score[ii], pi = parent[ii], st = A.st[64 * blockIdx.x + lane];
+  const int32_t mbase = start - kMarkLo;
+  for (int t = lane; t < kMarkN; t += 64) lm[t] = 0;
+  __syncthreads();
+  int32_t M = (int32_t)(yi >> 32 & 0xff), J = -1, N = 0;
+  uint64_t marks = 0;
+  bool act = mine;
+  uint32_t vis = 0;
+  constexpr int U = 4;  // candidates loaded per batch (their loads overlap)
+  for (int k0 = 0; k0 < 64; k0 += U) {
+    if (!__builtin_amdgcn_ballot_w64(act & (i - 1 - k0 >= st))) break;
+    uint64_t xj[U], yj[U];
+    int32_t fj[U], pj[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int32_t j = i - 1 - k0 - u;
+      xj[u] = yj[u] = 0;
+      fj[u] = 0;
+      pj[u] = -1;
+      if (act & (j >= st)) {
+        xj[u] = X[j];
+        yj[u] = Y[j];
+        fj[u] = score[j];
+        pj[u] = parent[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = k0 + u;
+      const int32_t j = i - 1 - k;
+      act = act & (j >= st);  // the window is exhausted: the loop ends
+      int32_t sg;
+      const bool ok = geometry(xi, yi, xj[u], yj[u], act, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+      vis += act ? 1u : 0u;
+      const int32_t sc = ok ? (int32_t)((uint32_t)sg + (uint32_t)fj[u]) : INT_MIN;
+      const bool upd = sc > M;  // false when filtered (M >= 0 > INT_MIN)
+      bool brk = false;
+      if (upd) {
+        M = sc;
+        J = j;
+        N = N > 0 ? N - 1 : 0;
+      } else if (ok & (bool)((marks >> k) & 1)) {
+        brk = ++N > kMaxSkip;  // host_kernel.cpp:84-88: the break skips the mark below
+      }
+      if (ok & !brk & (pj[u] >= 0)) {  // targets[parents[j]] = i (host_kernel.cpp:89)
+        const int32_t d = i - 1 - pj[u];
+        if (d < 64) marks |= 1ull << d;
+        const uint32_t o = (uint32_t)(pj[u] - mbase);
+        if (o < (uint32_t)kMarkN)
+          atomicMax(&lm[o], i);
+        else
+          atomicMax(tgt + pj[u], i);
+      }
+      act = act & !brk;
+    }
+  }
+  __syncthreads();
+  for (int t = lane; t < kMarkN; t += 64) {
+    const int32_t v = lm[t];
+    if (v) atomicMax(tgt + mbase + t, v);
+  }
+  // still scanning after 64 candidates with more in the window: verify_kernel takes the anchor
+  const bool unres = act & (i - 65 >= st);
+  const uint64_t um = __builtin_amdgcn_ballot_w64(unres);
+  const bool done = mine & !unres;
+  const uint64_t bad = __builtin_amdgcn_ballot_w64(CHECK & done & ((M != fi) | (J != pi)));
+  // visited pairs of the decided anchors (the undecided ones are counted by verify_kernel)
+  uint32_t v = done ? vis : 0u;
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) {
+    need[blockIdx.x] = um;
+    if (CHECK && bad) atomicMin(A.fail + ch.sc, start + (int32_t)__builtin_ctzll(bad));
+    if (v) atomicAdd(A.viscall + ch.sc, (unsigned long long)v);
   }
 }
 
@@ -537,6 +651,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   if (!st) st = grow(&B->d_front, &B->cap_front, 2 * ns);
   if (!st) st = grow(&B->d_viscall, &B->cap_viscall, ns);
   if (!st) st = grow(&B->d_t2, &B->cap_t2, B->nanchors);
+  if (!st) st = grow(&B->d_need, &B->cap_need, nch);
   if (st) return st;
   B->d_fail = B->d_front + ns;
   {
@@ -573,6 +688,9 @@ int split_resolve(gb_chain_batch *B) {
   GB_HIP(hipMemsetAsync(B->d_viscall, 0, (size_t)ns * 8, B->stream));
   const SplitArgs A = split_args(B);
   const int rounds = jump_rounds(B->max_split_n);
+  // GB_CHAIN_VLANES=0: verify_kernel alone (A/B and tests)
+  const char *vl = getenv("GB_CHAIN_VLANES");
+  const bool lanes = !(vl && vl[0] == '0');
   std::vector<VCall> fix;
   std::vector<uint8_t> failed((size_t)ns, 0);
   B->spec_rounds = 0;
@@ -583,7 +701,12 @@ int split_resolve(gb_chain_batch *B) {
     const int r = jump(B, 0, rounds);
     hipLaunchKernelGGL(guess_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
     GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
-    hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A);
+    if (lanes) {
+      hipLaunchKernelGGL(verify_lanes<true>, dim3(nch), dim3(64), 0, B->stream, A, B->d_need);
+      hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
+    } else {
+      hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)nullptr);
+    }
     GB_HIP(hipGetLastError());
     GB_HIP(hipMemcpyAsync(fail.data(), B->d_fail, (size_t)ns * 4, hipMemcpyDeviceToHost, B->stream));
     GB_HIP(hipStreamSynchronize(B->stream));
@@ -623,7 +746,12 @@ int split_resolve(gb_chain_batch *B) {
   }
   if (redo) {
     GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
-    hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A);
+    if (lanes) {
+      hipLaunchKernelGGL(verify_lanes<false>, dim3(nch), dim3(64), 0, B->stream, A, B->d_need);
+      hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
+    } else {
+      hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)nullptr);
+    }
     GB_HIP(hipStreamSynchronize(B->stream));  // `front` is a host vector about to go
   }
   hipLaunchKernelGGL(peak_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
@@ -638,7 +766,7 @@ void split_free(gb_chain_batch *B) {
   for (void *p : {(void *)B->d_vc, (void *)B->d_split, (void *)B->d_segs, (void *)B->d_chunks, (void *)B->d_st,
                   (void *)B->d_sscore, (void *)B->d_sparent, (void *)B->d_front, (void *)B->d_link[0],
                   (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1], (void *)B->d_t2,
-                  (void *)B->d_viscall, (void *)B->d_smark})
+                  (void *)B->d_viscall, (void *)B->d_smark, (void *)B->d_need})
     (void)hipFree(p);
   B->d_vc = nullptr;
 }

@@ -174,6 +174,25 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault, rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split,fault", [("", 0), ("128,8", 37)])
+def test_gpu_split_wave_verification(split_calls, monkeypatch, split, fault):
+    """GB_CHAIN_VLANES=0: every split anchor verified by verify_kernel (64 lanes per candidate block)
+    instead of verify_lanes (one lane per anchor, verify_kernel only for loops past 64 candidates)."""
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    calls, exp = split_calls
+    monkeypatch.setenv("GB_CHAIN_SPLIT", split)
+    monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
+    monkeypatch.setenv("GB_CHAIN_VLANES", "0")
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
+    b.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("split,fault", [("512,64", 53), ("1024,0", 211)])
 def test_gpu_split_remark_wide_windows(monkeypatch, split, fault):
     """Calls whose windows hold up to max_iter (5000) anchors and whose parent links reach far back,
