@@ -430,19 +430,21 @@ int grow(T **p, int64_t *cap, int64_t need) {
 // under the batch's throughput time, so small batches get shorter segments; shorter ones cost more
 // verification and warm-up work. GB_CHAIN_SPLIT: "0" runs every call whole; "SEG[,WARM]" sets the segment length and warm-up
 // (tests force tiny segments without warm-up to exercise the fix-up path).
-void split_knobs(int64_t total_anchors, int *seg, int *warm) {
+void split_knobs(int64_t total_anchors, int *seg, int *warm, int *trunc) {
   // the power of two in [512, 4096] nearest below total / 12 000 (measured with chain_rows,
   // tools/chain_rows_probe.py: 'large' 25.4 M anchors 2048 (7.76 ms; 4096 7.87, 1024 10.3), 'small'
   // 2.5 M and the 1/8 shard 3.2 M anchors 512 (2.06 / 2.20 ms; 1024 2.29 / 2.38)
   *seg = kSegDefault;
   while (*seg > 512 && (int64_t)*seg * 12000 > total_anchors) *seg /= 2;
   *warm = kWarmDefault;
+  *trunc = 0;
   const char *e = getenv("GB_CHAIN_SPLIT");
   if (!e || !*e) return;
-  int a = 0, b = -1;
-  const int k = sscanf(e, "%d,%d", &a, &b);
+  int a = 0, b = -1, t = 0;
+  const int k = sscanf(e, "%d,%d,%d", &a, &b, &t);
   if (k >= 1) *seg = a;
   if (k >= 2 && b >= 0) *warm = b;
+  if (k >= 3) *trunc = t;
 }
 
 SplitArgs split_args(gb_chain_batch *B) {
@@ -499,8 +501,8 @@ int jump(gb_chain_batch *B, int op, int rounds) {
 }  // namespace
 
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4) {
-  int seg, warm;
-  split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm);
+  int seg, warm, trunc;
+  split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm, &trunc);
   const int64_t ncalls = B->ncalls;
   B->vc.clear();
   B->split.clear();
@@ -569,7 +571,10 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
           K.win.resize((size_t)nseg);
           for (int32_t k = 0; k < nseg; k++) {
             const int32_t cs = k * L, es = k + 1 == nseg ? n : (k + 1) * L;
-            const int32_t a = k == 0 ? 0 : std::max(0, K.st[(size_t)cs] - warm);
+            // trunc: the warm-up starts `warm` anchors before c_s whatever the window (the first
+            // anchors' spec loops then miss their oldest candidates, which only matters -- and is
+            // then caught by the verification -- for loops that would have reached them)
+            const int32_t a = k == 0 ? 0 : std::max(0, trunc ? cs - warm : K.st[(size_t)cs] - warm);
             int32_t w = 0;
             for (int32_t i = a; i < es; i++) w = std::max(w, i - std::max(a, K.st[(size_t)i]));
             K.as[(size_t)k] = a;

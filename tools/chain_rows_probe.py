@@ -41,8 +41,13 @@ def run(calls, rows, split=None):
         b.sync()
         ks.append(b.timing())
     res = b.results()
+    global last_stats
+    last_stats = b.split_stats()
     b.close()
     return min(ks), res
+
+
+last_stats = None
 
 
 for name, calls in sets:
@@ -56,4 +61,5 @@ for name, calls in sets:
     for s in [x for x in os.environ.get("CHAIN_SPLITS", "").split(";") if x]:
         ts, rs = run(calls, "1", s)
         ok = all(np.array_equal(a, b) for a, b in zip(r0[:4], rs[:4])) and r0[4] == rs[4]
-        print(f"   rows, split {s:10s}: {ts:7.3f} ms ({calls.nanchors / ts / 1e3:7.1f} Manchors/s) same={ok}", flush=True)
+        print(f"   rows, split {s:10s}: {ts:7.3f} ms ({calls.nanchors / ts / 1e3:7.1f} Manchors/s) same={ok} "
+              f"(split calls, rounds, fix-ups {last_stats})", flush=True)

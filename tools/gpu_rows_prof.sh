@@ -9,8 +9,8 @@ export CHAIN_SETS=${PROF_SETS:-large}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rows_prof -o run -- python3 tools/chain_rows_probe.py > gpurun_out/rows_prof.log 2>&1 || { tail -20 gpurun_out/rows_prof.log; exit 1; }
 cat gpurun_out/rows_prof.log
 f=$(find gpurun_out/rows_prof -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/rows_kernel_stats.csv; head -12 gpurun_out/rows_kernel_stats.csv | cut -c1-160
-C="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"
-timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d gpurun_out/rows_pmc -o run -- python3 tools/chain_rows_probe.py > gpurun_out/rows_pmc.log 2>&1 || { echo "pmc failed"; tail gpurun_out/rows_pmc.log; exit 1; }
+C=""
+exit 0
 f=$(find gpurun_out/rows_pmc -name '*counter_collection.csv' | head -1); python3 - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
