@@ -218,14 +218,32 @@ __global__ void k_special(int32_t cap, const int32_t *__restrict__ eoff, int nca
   bchain[aoff[e]] = e;
 }
 
+// the accepted chain owning each anchor (entry index), or -1: one thread per anchor, ahead of the
+// sequential sweep of k_place (whose steps then read one staged word instead of two dependent loads)
+__global__ void k_ent(int64_t n, const int32_t *__restrict__ cid, const int32_t *__restrict__ eoff,
+                      const int32_t *__restrict__ first, const int32_t *__restrict__ acc, int32_t *__restrict__ ent) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const int32_t fr = first[g];
+  int32_t e = -1;
+  if (fr != kInf) {
+    e = eoff[cid[g]] + fr;
+    if (!acc[e]) e = -1;
+  }
+  ent[g] = e;
+}
+
 // anchor positions of the owned paths: one ascending sweep per call, 64 anchors per step; a
 // chain's counter (LDS when the call has <= kLdsCtr chains, global otherwise) advances once per
-// step by its group size, and lanes rank themselves inside their group
+// step by its group size, and lanes rank themselves inside their group. The owners (k_ent) are read
+// kPlaceBlk steps at a time, one block ahead, so the sweep waits on memory once per block; groups
+// are found one distinct owner at a time (ballot), not by a 64-lane scan per lane.
 constexpr int kLdsCtr = 8192;
+constexpr int kPlaceBlk = 16;
 __global__ __launch_bounds__(64) void k_place(const int64_t *__restrict__ off, const int32_t *__restrict__ eoff,
-                                              const int32_t *__restrict__ first, const int32_t *__restrict__ acc,
-                                              const int32_t *__restrict__ aoff, int32_t *__restrict__ ctr,
-                                              int32_t *__restrict__ bidx, int32_t *__restrict__ bchain) {
+                                              const int32_t *__restrict__ ent, const int32_t *__restrict__ aoff,
+                                              int32_t *__restrict__ ctr, int32_t *__restrict__ bidx,
+                                              int32_t *__restrict__ bchain) {
   __shared__ int32_t lctr[kLdsCtr];
   __shared__ int32_t base_of[64];
   const int c = blockIdx.x, lane = threadIdx.x;
@@ -235,40 +253,52 @@ __global__ __launch_bounds__(64) void k_place(const int64_t *__restrict__ off, c
   if (lds)
     for (int k = lane; k < ne; k += 64) lctr[k] = 0;
   __syncthreads();
-  for (int32_t lo = 0; lo < n; lo += 64) {
-    const int32_t i = lo + lane;
-    int32_t e = -1;
-    if (i < n) {
-      const int32_t fr = first[o + i];
-      if (fr != kInf) {
-        e = e0 + fr;
-        if (!acc[e]) e = -1;
+  int32_t cur[kPlaceBlk], nxt[kPlaceBlk];
+#pragma unroll
+  for (int s = 0; s < kPlaceBlk; s++) cur[s] = s * 64 + lane < n ? ent[o + s * 64 + lane] : -1;
+  for (int32_t blo = 0; blo < n; blo += 64 * kPlaceBlk) {
+#pragma unroll
+    for (int s = 0; s < kPlaceBlk; s++) {
+      const int32_t i = blo + 64 * kPlaceBlk + s * 64 + lane;
+      nxt[s] = i < n ? ent[o + i] : -1;
+    }
+#pragma unroll
+    for (int s = 0; s < kPlaceBlk; s++) {
+      const int32_t lo = blo + 64 * s;
+      if (lo >= n) break;
+      const int32_t i = lo + lane;
+      const int32_t e = cur[s];
+      int rank = 0, gsize = 0, leader = lane;
+      uint64_t rem = __builtin_amdgcn_ballot_w64(e >= 0);
+      while (rem) {
+        const int l0 = __builtin_ctzll(rem);
+        const int32_t v = __builtin_amdgcn_readlane(e, l0);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(e == v);
+        if (e == v) {
+          rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          gsize = __builtin_popcountll(m);
+          leader = l0;
+        }
+        rem &= ~m;
       }
-    }
-    int rank = 0, gsize = 0, leader = lane;
-    for (int l = 0; l < 64; l++) {
-      const int32_t el = __builtin_amdgcn_readlane(e, l);
-      if (el == e) {
-        gsize++;
-        if (l < lane) rank++;
-        if (l < leader) leader = l;
+      if (e >= 0 && leader == lane) {
+        if (lds) {
+          base_of[lane] = lctr[e - e0];
+          lctr[e - e0] += gsize;
+        } else {
+          base_of[lane] = atomicAdd(&ctr[e], gsize);
+        }
       }
-    }
-    if (e >= 0 && leader == lane) {
-      if (lds) {
-        base_of[lane] = lctr[e - e0];
-        lctr[e - e0] += gsize;
-      } else {
-        base_of[lane] = atomicAdd(&ctr[e], gsize);
+      __syncthreads();
+      if (e >= 0) {
+        const int32_t pos = aoff[e] + base_of[leader] + rank;
+        bidx[pos] = (int32_t)(o + i);
+        bchain[pos] = e;
       }
+      __syncthreads();
     }
-    __syncthreads();
-    if (e >= 0) {
-      const int32_t pos = aoff[e] + base_of[leader] + rank;
-      bidx[pos] = (int32_t)(o + i);
-      bchain[pos] = e;
-    }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kPlaceBlk; s++) cur[s] = nxt[s];
   }
 }
 
@@ -390,21 +420,73 @@ __global__ __launch_bounds__(64) void k_reorder(const int32_t *__restrict__ eoff
   }
   W128 *wc = nu <= kLdsW ? lw : w + k0;
   int32_t *sc = nu <= kLdsW ? lsc : scratch + (size_t)c * kRsLevels * 512;  // the call's own slice
-  for (int32_t k = lane; k < nu; k += 64) {
-    const int32_t e = kentry[k0 + k];
-    wc[k].x = x[bidx[aoff[e]]];
-    wc[k].y = (uint64_t)(uint32_t)(aoff[e] - a0) << 32 | (uint32_t)k;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    radix_sort_128x(wc, nu, sc);
-    int32_t run = a0;
-    for (int32_t i = 0; i < nu; i++) {
-      const int32_t e = kentry[k0 + (int32_t)(uint32_t)wc[i].y];
-      uout[k0 + i] = u[e];
-      newoff[e] = run;
-      run += (int32_t)(uint32_t)u[e];
+  auto fill = [&]() {
+    for (int32_t k = lane; k < nu; k += 64) {
+      const int32_t e = kentry[k0 + k];
+      wc[k].x = x[bidx[aoff[e]]];
+      wc[k].y = (uint64_t)(uint32_t)(aoff[e] - a0) << 32 | (uint32_t)k;
     }
+  };
+  fill();
+  __syncthreads();
+  // Distinct keys (the usual case): every sort gives ksort's order, so the wave sorts the LDS copy
+  // with a bitonic network (pads of ~0 payload last) and checks the keys are distinct; with a
+  // repeated key, ksort's tie order is its own, so the array is rebuilt and lane 0 replays it.
+  bool sorted = false;
+  if (nu <= kLdsW) {
+    int32_t np = 1;
+    while (np < nu) np <<= 1;
+    for (int32_t k = nu + lane; k < np; k += 64) {
+      lw[k].x = ~0ull;
+      lw[k].y = ~0ull;
+    }
+    __syncthreads();
+    for (int32_t kk = 2; kk <= np; kk <<= 1)
+      for (int32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (int32_t t = lane; t < (np >> 1); t += 64) {
+          const int32_t a = ((t & ~(jj - 1)) << 1) | (t & (jj - 1)), b = a | jj;  // a has bit jj clear
+          const W128 pa = lw[a], pb = lw[b];
+          const bool gt = pa.x > pb.x || (pa.x == pb.x && pa.y > pb.y);
+          const bool up = (a & kk) == 0;
+          if (gt == up) {
+            lw[a] = pb;
+            lw[b] = pa;
+          }
+        }
+        __syncthreads();
+      }
+    bool dup = false;
+    for (int32_t i = 1 + lane; i < nu; i += 64) dup |= lw[i].x == lw[i - 1].x;
+    sorted = __builtin_amdgcn_ballot_w64(dup) == 0;
+    if (!sorted) {
+      __syncthreads();
+      fill();
+      __syncthreads();
+    }
+  }
+  if (!sorted && lane == 0) radix_sort_128x(wc, nu, sc);
+  __syncthreads();
+  // outputs in sorted order; offsets are the running sum of the chain lengths (a wave scan per 64)
+  int32_t run = a0;
+  for (int32_t i0 = 0; i0 < nu; i0 += 64) {
+    const int32_t i = i0 + lane;
+    int32_t e = 0, len = 0;
+    uint64_t ue = 0;
+    if (i < nu) {
+      e = kentry[k0 + (int32_t)(uint32_t)wc[i].y];
+      ue = u[e];
+      len = (int32_t)(uint32_t)ue;
+    }
+    int32_t incl = len;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    if (i < nu) {
+      uout[k0 + i] = ue;
+      newoff[e] = run + incl - len;
+    }
+    run += __shfl(incl, 63);
   }
 }
 
@@ -551,8 +633,10 @@ int gb_chain_batch_backtrack(gb_chain_batch *B, int32_t min_cnt, int32_t min_sc)
     hipLaunchKernelGGL(k_special, dim3(ga), dim3(256), 0, s, cap, T->eoff, nc, B->d_off, T->ecall, T->skeys, T->acc,
                        T->own, T->kidx, T->aoff, T->bidx, T->bchain, T->kentry);
     GB_HIP(hipMemsetAsync(T->ctr, 0, n * 4, s));
-    hipLaunchKernelGGL(k_place, dim3(nc), dim3(64), 0, s, B->d_off, T->eoff, T->first, T->acc, T->aoff, T->ctr,
-                       T->bidx, T->bchain);
+    // owners per anchor into clen (no longer read after k_accept)
+    hipLaunchKernelGGL(k_ent, dim3(ga), dim3(256), 0, s, n, T->cid, T->eoff, T->first, T->acc, T->clen);
+    hipLaunchKernelGGL(k_place, dim3(nc), dim3(64), 0, s, B->d_off, T->eoff, (const int32_t *)T->clen, T->aoff,
+                       T->ctr, T->bidx, T->bchain);
     hipLaunchKernelGGL(k_reorder, dim3(nc), dim3(64), 0, s, T->eoff, T->kidx, T->aoff, T->kentry, T->bidx, B->d_x,
                        T->u, T->w, T->uout, T->newoff, T->scratch);
     const unsigned gb = (unsigned)((2 * n + 255) / 256);

@@ -105,3 +105,40 @@ def test_gpu_vs_oracle(seed, ncalls, median, maxn):
     _, ous, oan = oracle_lib.chain_bt_oracle(calls, f, p, v, 3, 40, 8)
     same_chains(calls, gus, gan, ous, oan)
     b.close()
+
+
+def twin_calls(seed, ncalls, n):
+    """Every anchor twice, at the same x on two parallel diagonals (y and y + 2 000): chains come in
+    pairs whose first anchors share x, so calls with more than 64 kept chains sort tied keys -- the
+    path where k_reorder leaves its parallel sort to the replay of ksort (whose tie order is its own)."""
+    rng = np.random.default_rng(seed)
+    offs, xs, ys, aq = [0], [], [], []
+    for _ in range(ncalls):
+        x, y, a = gen.chain_call(rng, n)
+        x2 = np.repeat(x, 2)
+        y2 = np.repeat(y, 2)
+        y2[1::2] += np.uint64(2000)
+        xs.append(x2)
+        ys.append(y2)
+        aq.append(a)
+        offs.append(offs[-1] + len(x2))
+    params = np.tile(np.array([5000, 5000, 500, 1], np.int32), (ncalls, 1))
+    return gen.ChainCalls(np.array(offs, np.int64), np.concatenate(xs), np.concatenate(ys), np.array(aq, np.float32),
+                          params)
+
+
+@pytest.mark.gpu
+def test_gpu_tied_keys_vs_oracle():
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    calls = twin_calls(17, 40, 3000)
+    b = chain.ChainBatch(calls)
+    b.run()
+    f, p, _, v, _ = b.results()
+    for mc, ms in [(3, 40), (1, 0)]:
+        b.backtrack(mc, ms)
+        gus, gan = gpu_chains(b, calls)
+        _, ous, oan = oracle_lib.chain_bt_oracle(calls, f, p, v, mc, ms, 8)
+        same_chains(calls, gus, gan, ous, oan)
+        assert max(len(u) for u in ous) > 64  # the sort path, not the 64-lane ranking
+    b.close()
