@@ -105,6 +105,10 @@ __global__ void k_rank(int32_t cap, const int32_t *__restrict__ eoff, int ncalls
 // with every child beyond the current chunk; inside the chunk the subtree minima come from six
 // doubling rounds (round k folds in the descendants 2^k links down, by LDS atomicMin on the 2^k-th
 // ancestor), then each chunk node whose parent lies below the chunk folds its value into the ring.
+// The parents of a step's chunk and the ranks entering the window with it are loaded kFirstBlk
+// steps at a time, one block ahead (the sweep then waits on memory once per block, not twice per
+// step); the first step fills the whole window below the top chunk itself.
+constexpr int kFirstBlk = 16;
 __global__ __launch_bounds__(64) void k_first(const int64_t *__restrict__ off, const int32_t *__restrict__ par,
                                               const int32_t *__restrict__ rank, int32_t *__restrict__ first) {
   __shared__ int32_t ring[kWin];
@@ -113,16 +117,47 @@ __global__ __launch_bounds__(64) void k_first(const int64_t *__restrict__ off, c
   const int64_t o = off[c];
   const int32_t n = (int32_t)(off[c + 1] - o);
   if (n == 0) return;
-  int32_t init_lo = n;  // ring holds indices [init_lo, ...)
-  for (int32_t hi = n - 1; hi >= 0; hi -= 64) {
-    const int32_t lo = max(hi - 63, 0);
-    const int32_t need = max(lo - kParentWindow, 0);
-    for (int32_t k = init_lo - 1 - lane; k >= need; k -= 64) ring[k & (kWin - 1)] = rank[o + k];
-    init_lo = min(init_lo, need);
+  const int32_t nsteps = (n + 63) / 64;
+  auto lo_of = [&](int32_t t) { return max(n - 64 * (t + 1), 0); };
+  auto need_of = [&](int32_t t) { return max(lo_of(t) - kParentWindow, 0); };
+  // step t's parents (lane: anchor lo + lane) and new window ranks (lane: anchor need_t + lane)
+  auto load_block = [&](int32_t t0, int32_t *P, int32_t *R) {
+#pragma unroll
+    for (int s = 0; s < kFirstBlk; s++) {
+      const int32_t t = t0 + s;
+      P[s] = -1;
+      R[s] = kInf;
+      if (t < nsteps) {
+        const int32_t lo = lo_of(t), hi = n - 1 - 64 * t, i = lo + lane;
+        if (i <= hi) P[s] = par[o + i];
+        if (t > 0) {
+          const int32_t k = need_of(t) + lane;
+          if (k < need_of(t - 1)) R[s] = rank[o + k];
+        }
+      }
+    }
+  };
+  {  // step 0's window: [need_0, n)
+    const int32_t need0 = need_of(0);
+    for (int32_t k = n - 1 - lane; k >= need0; k -= 64) ring[k & (kWin - 1)] = rank[o + k];
+  }
+  int32_t cp[kFirstBlk], cr[kFirstBlk], np[kFirstBlk], nr[kFirstBlk];
+  load_block(0, cp, cr);
+  for (int32_t t0 = 0; t0 < nsteps; t0 += kFirstBlk) {
+    load_block(t0 + kFirstBlk, np, nr);
+#pragma unroll
+    for (int s = 0; s < kFirstBlk; s++) {
+    const int32_t t = t0 + s;
+    if (t >= nsteps) break;
+    const int32_t hi = n - 1 - 64 * t, lo = lo_of(t);
+    if (t > 0) {
+      const int32_t k = need_of(t) + lane;
+      if (k < need_of(t - 1)) ring[k & (kWin - 1)] = cr[s];
+    }
     __syncthreads();
     const int32_t i = lo + lane;
     const bool live = i <= hi;
-    const int32_t pp = live ? par[o + i] : -1;
+    const int32_t pp = cp[s];
     int32_t m = live ? ring[i & (kWin - 1)] : kInf;
     int anc = (live && pp >= lo) ? pp - lo : -1;  // in-chunk parent (lane), or -1
 #pragma unroll
@@ -139,6 +174,12 @@ __global__ __launch_bounds__(64) void k_first(const int64_t *__restrict__ off, c
     if (live && pp >= 0 && pp < lo) atomicMin(&ring[pp & (kWin - 1)], m);
     if (live) first[o + i] = m;
     __syncthreads();
+    }
+#pragma unroll
+    for (int s = 0; s < kFirstBlk; s++) {
+      cp[s] = np[s];
+      cr[s] = nr[s];
+    }
   }
 }
 
