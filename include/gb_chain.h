@@ -39,8 +39,11 @@ int gb_chain_batch_timing(gb_chain_batch *b, float *kernel_ms);
 /* Diagnostics of the last run: calls run as speculative segments (long calls with sorted x, see
  * csrc/chain_split.hip), guess/verify rounds, and fix-up blocks (anchors whose guess failed the
  * verification and were recomputed sequentially). Environment (development aids, read when a batch
- * is filled): GB_CHAIN_SPLIT = "0" (no splitting) or "SEG[,WARM]"; GB_CHAIN_SPLIT_FAULT = k makes
- * the guess of every k-th anchor wrong (read at run time), to exercise the verification. */
+ * is filled): GB_CHAIN_SPLIT = "0" (no splitting) or "SEG[,WARM[,1]]" (1: warm-up from the
+ * segment start, not its window); GB_CHAIN_SPLIT_FAULT = k makes the guess of every k-th anchor
+ * wrong (read at run time), to exercise the verification; GB_CHAIN_ROWS=0 runs every block on the
+ * 64-lane sequential kernel instead of chain_rows (two calls per wave), GB_CHAIN_VLANES=0 verifies
+ * every split anchor with the 64-lane verification instead of one anchor per lane (A/B, tests). */
 int gb_chain_batch_split_stats(gb_chain_batch *b, int64_t *split_calls, int64_t *rounds, int64_t *fixups);
 int gb_chain_batch_destroy(gb_chain_batch *b);
 
