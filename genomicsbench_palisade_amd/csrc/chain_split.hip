@@ -118,22 +118,26 @@ __global__ __launch_bounds__(256) void jump_round(int64_t n, const int32_t *li, 
   vo[j] = v;
 }
 
-// Links inside one 64-entry chunk first: six doubling rounds in LDS leave every entry with its first
-// link outside its chunk (links point to earlier anchors) and the value folded up to it, so the
-// global rounds that follow count hops between chunks, not anchors (ceil(log2(chunks)) + 1 rounds).
+// Links inside one kTile-entry tile of the chunk space first: log2(kTile) doubling rounds in LDS
+// leave every entry with its first link outside its tile (links point to earlier anchors of the same
+// call) and the value folded up to it, so the global rounds that follow count hops between tiles,
+// not anchors: a path of a call of n split anchors crosses at most n / kTile + 2 tiles.
+constexpr int kTile = 1024, kTileLog = 10;
 template <int OP>
-__global__ __launch_bounds__(64) void jump_local(int32_t *link, int32_t *val) {
-  __shared__ int32_t ll[2][64], lv[2][64];
-  const int32_t base = 64 * (int32_t)blockIdx.x, t = (int32_t)threadIdx.x;
-  ll[0][t] = link[base + t];
-  lv[0][t] = val[base + t];
+__global__ __launch_bounds__(kTile) void jump_local(int64_t nj, int32_t *link, int32_t *val) {
+  __shared__ int32_t ll[2][kTile], lv[2][kTile];
+  const int64_t base = (int64_t)kTile * blockIdx.x;
+  const int32_t t = (int32_t)threadIdx.x;
+  const bool in = base + t < nj;
+  ll[0][t] = in ? link[base + t] : -1;
+  lv[0][t] = in ? val[base + t] : 0;
   __syncthreads();
   int cur = 0;
 #pragma unroll
-  for (int r = 0; r < 6; r++) {
+  for (int r = 0; r < kTileLog; r++) {
     const int32_t l = ll[cur][t];
     int32_t v = lv[cur][t], nl = l;
-    if (l >= base && l < base + 64) {
+    if (l >= base && l < base + kTile) {
       const int32_t w = lv[cur][l - base];
       v = OP == 0 ? v + w : max(v, w);
       nl = ll[cur][l - base];
@@ -143,8 +147,10 @@ __global__ __launch_bounds__(64) void jump_local(int32_t *link, int32_t *val) {
     __syncthreads();
     cur ^= 1;
   }
-  link[base + t] = ll[cur][t];
-  val[base + t] = lv[cur][t];
+  if (in) {
+    link[base + t] = ll[cur][t];
+    val[base + t] = lv[cur][t];
+  }
 }
 
 __global__ __launch_bounds__(64) void guess_write(SplitArgs A, const int32_t *val) {
@@ -514,11 +520,11 @@ int jump_rounds(int n) {
 int jump(gb_chain_batch *B, int op, int rounds) {
   const int64_t nj = 64 * (int64_t)B->chunks.size();
   const unsigned g = (unsigned)((nj + 255) / 256);
-  const unsigned nch = (unsigned)B->chunks.size();
+  const unsigned nt = (unsigned)((nj + kTile - 1) / kTile);
   if (op == 0)
-    hipLaunchKernelGGL(jump_local<0>, dim3(nch), dim3(64), 0, B->stream, B->d_link[0], B->d_val[0]);
+    hipLaunchKernelGGL(jump_local<0>, dim3(nt), dim3(kTile), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
   else
-    hipLaunchKernelGGL(jump_local<1>, dim3(nch), dim3(64), 0, B->stream, B->d_link[0], B->d_val[0]);
+    hipLaunchKernelGGL(jump_local<1>, dim3(nt), dim3(kTile), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
   int cur = 0;
   for (int r = 0; r < rounds; r++) {
     if (op == 0)
@@ -726,8 +732,8 @@ int split_resolve(gb_chain_batch *B) {
   GB_HIP(hipMemsetAsync(B->d_t2, 0, (size_t)B->nanchors * 4, B->stream));
   GB_HIP(hipMemsetAsync(B->d_viscall, 0, (size_t)ns * 8, B->stream));
   const SplitArgs A = split_args(B);
-  // global rounds after jump_local: hops between 64-anchor chunks
-  const int rounds = jump_rounds(B->max_split_n / 64 + 1);
+  // global rounds after jump_local: hops between tiles
+  const int rounds = jump_rounds(B->max_split_n / kTile + 2);
   // GB_CHAIN_VLANES=0: verify_kernel alone (A/B and tests)
   const char *vl = getenv("GB_CHAIN_VLANES");
   const bool lanes = !(vl && vl[0] == '0');
