@@ -302,12 +302,14 @@ def physical_cores():
     return len(seen) or None
 
 
-def add_per_core(obj, cores_all=None):
-    """cpu_baseline objects (nested ones too) get value per thread used and the all-core estimate
-    of BASELINE.md section 3 (per thread x every logical CPU of the host: an upper bound for the CPU,
-    SMT siblings do not double a core's rate)."""
+def add_per_core(obj, cores_all=None, cores_phys=None):
+    """cpu_baseline objects (nested ones too) get value per thread used and the all-core estimates
+    of BASELINE.md section 3: per thread x every logical CPU of the host (an upper bound for the CPU,
+    SMT siblings do not double a core's rate) and per thread x the physical cores."""
     if cores_all is None:
         cores_all = os.cpu_count()
+    if cores_phys is None:
+        cores_phys = physical_cores()
     if isinstance(obj, dict):
         if "cpu_baseline" in obj and isinstance(obj["cpu_baseline"], dict):
             cb = obj["cpu_baseline"]
@@ -315,10 +317,113 @@ def add_per_core(obj, cores_all=None):
                 cb["per_core"] = cb["value"] / cb["cores"]
                 if cores_all:
                     cb["all_core_estimate"] = {"value": cb["per_core"] * cores_all, "cores": cores_all}
+                if cores_phys:
+                    cb["all_core_estimate_physical"] = {"value": cb["per_core"] * cores_phys, "cores": cores_phys}
             if isinstance(cb.get("port"), dict) and cb["port"].get("value") and cb["port"].get("cores"):
                 cb["port"]["per_core"] = cb["port"]["value"] / cb["port"]["cores"]
         for v in obj.values():
-            add_per_core(v, cores_all)
+            add_per_core(v, cores_all, cores_phys)
+
+
+HEADLINE_MAX_BYTES = 4096
+
+
+def _sig(x, n=4):
+    """x rounded to n significant digits (floats only), for the compact headline."""
+    if isinstance(x, float):
+        if x == 0 or x != x:
+            return x
+        from math import floor, log10
+        return round(x, max(0, n - 1 - int(floor(log10(abs(x))))))
+    return x
+
+
+def _pick(d, keys):
+    if not isinstance(d, dict):
+        return None
+    return {k: _sig(d[k]) for k in keys if k in d and d[k] is not None}
+
+
+def _cpu_short(cb):
+    if not isinstance(cb, dict):
+        return None
+    out = _pick(cb, ("value", "unit", "cores", "kind", "per_core"))
+    pc = cb.get("parity_check") or {}
+    if "bit_exact" in pc:
+        out["bit_exact"] = bool(pc["bit_exact"])
+    for k, short in (("all_core_estimate", "all_core_logical"), ("all_core_estimate_physical", "all_core_physical")):
+        if isinstance(cb.get(k), dict):
+            out[short] = [_sig(cb[k]["value"]), cb[k]["cores"]]
+    return out
+
+
+def _roof_short(r):
+    out = _pick(r, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic"))
+    if out and isinstance(out.get("kernel"), str):
+        out["kernel"] = out["kernel"].split(" ")[0]
+    return out
+
+
+def _leg_short(leg):
+    if not isinstance(leg, dict):
+        return None
+    out = _pick(leg, ("value", "unit", "ms_per_step"))
+    wl = (leg.get("config") or {}).get("workload")
+    if isinstance(wl, str):
+        import re
+        out["workload"] = re.sub(r" \([^)]*\)", "", wl.split(";")[0])[:100]
+    out["roofline"] = _roof_short(leg.get("roofline"))
+    out["cpu_baseline"] = _cpu_short(leg.get("cpu_baseline"))
+    sp = leg.get("shard_proxy")
+    if isinstance(sp, dict):
+        out["shard_proxy"] = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
+                              "speedup": _sig(sp.get("projected_speedup"))}
+    return out
+
+
+def headline(line: dict, detail_path=None) -> dict:
+    """The one compact JSON line the driver parses (<= HEADLINE_MAX_BYTES): the contract's fields, the
+    phmm headline's roofline and cpu_baseline, and per leg (fmi, chain, bsw, + chain backtrack, fmi
+    human-scale and the 'small' values) value / ms_per_step / workload / roofline / cpu_baseline.
+    Everything else (shard proxies' per-rank times, drop-ins, traffic_detail, parity-check objects)
+    goes to the detail file named in `detail`."""
+    h = {k: line.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    h["value"] = _sig(h["value"], 6)
+    cfg = line.get("config") or {}
+    h["config"] = {"workload": cfg.get("workload"), "parallelism": cfg.get("parallelism")}
+    h["roofline"] = _roof_short(line.get("roofline"))
+    h["cpu_baseline"] = _cpu_short(line.get("cpu_baseline"))
+    sp = line.get("shard_proxy")
+    if isinstance(sp, dict):
+        h["shard_proxy"] = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
+                            "speedup": _sig(sp.get("projected_speedup"))}
+    if isinstance(line.get("roofline_f64"), dict):
+        h["roofline_f64_frac"] = _sig(line["roofline_f64"].get("frac"))
+    for leg in ("fmi", "chain", "bsw"):
+        h[leg] = _leg_short(line.get(leg))
+    fm, ch = line.get("fmi") or {}, line.get("chain") or {}
+    if isinstance(ch.get("backtrack"), dict):
+        h["chain"]["backtrack"] = _pick(ch["backtrack"], ("value", "unit"))
+        h["chain"]["backtrack"]["frac"] = _sig((ch["backtrack"].get("roofline") or {}).get("frac"))
+    if isinstance(fm.get("human"), dict):
+        hu = fm["human"]
+        h["fmi"]["human"] = _pick(hu, ("value", "unit"))
+        h["fmi"]["human"]["frac"] = _sig((hu.get("roofline") or {}).get("frac"))
+        h["fmi"]["human"]["rows"] = (hu.get("config") or {}).get("workload", "").split("BWT rows ")[-1].split(",")[0]
+    if isinstance(line.get("small"), dict):
+        h["small"] = {k: _sig(v.get("value")) for k, v in line["small"].items() if isinstance(v, dict)}
+    if detail_path:
+        h["detail"] = detail_path
+    # never let the line outgrow the driver's capture: drop the least important parts first
+    for drop in (("small",), ("fmi", "human"), ("chain", "backtrack"), ("data",)):
+        if len(json.dumps(h)) <= HEADLINE_MAX_BYTES:
+            break
+        tgt = h
+        for k in drop[:-1]:
+            tgt = tgt.get(k) or {}
+        tgt.pop(drop[-1], None)
+    return h
 
 
 def cpu_baseline_chain(calls, sample_seconds: float, gpu=None):
@@ -1335,6 +1440,9 @@ def main():
                     help="single-GPU proxy (world size 1, strong scaling): also time the shards an N-GPU run "
                          "would give its ranks (0 or 1 = off)")
     ap.add_argument("--shard-rank", type=int, default=-1, help="proxy only this rank's shard (-1 = every rank)")
+    ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                    help="where the full record goes (shard proxies, drop-ins, traffic detail, parity checks); "
+                         "stdout carries only the compact headline line ('' = no file)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -1383,9 +1491,7 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32+f64 (phmm), int64 (fmi), int32/f64 (chain), int32 (bsw)",
-            "data": f"synthetic ('large'-shaped PairHMM batches {seeds} 1; genome-like reference seed 7 + 151 bp "
-                    f"reads {seeds} 8 for fmi; minimap2-shaped anchor calls {seeds} 5 for chain; extension pairs "
-                    f"{seeds} 11 for bsw)",
+            "data": f"synthetic, 'large'-shaped ({seeds}: phmm 1, fmi genome 7 + reads 8, chain 5, bsw 11)",
             "config": {"workload": ("phmm large: %d batches, %d testcases, %.3f G cells per step (whole job); "
                                     "%s; %.1f%% of rank 0's testcases on the f64 fallback" % (
                                         args.batches, ph["ntc"], ph["cells"] / 1e9, ph["shard"], 100 * ph["f64_frac"]))
@@ -1404,7 +1510,14 @@ def main():
             "cpu_host": cpu_host() if not args.no_cpu_baseline else None,
         }
         add_per_core(line)
-        print(json.dumps(line))
+        detail = args.detail_out
+        if detail:
+            d = detail if os.path.isabs(detail) else os.path.join(ROOT, detail)
+            os.makedirs(os.path.dirname(d), exist_ok=True)
+            with open(d, "w") as f:
+                json.dump(line, f)
+            log(f"full bench record: {detail} ({len(json.dumps(line))} bytes)")
+        print(json.dumps(headline(line, detail)), flush=True)
     D.close()
 
 

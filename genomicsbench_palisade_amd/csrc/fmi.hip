@@ -121,7 +121,7 @@ struct SearchArgs {
   unsigned long long *bwt_calls;
   int32_t budget;        // a read still running after this many backwardExt calls is handed to the
                          // wave-cooperative pass (smem_heavy); INT32_MAX = never
-  int32_t *heavy;        // reads handed over (capacity nreads) and their count
+  int32_t *heavy;        // reads handed over, (read, big slot or -1) pairs (capacity nreads), and their count
   int32_t *heavy_n;
   int32_t prefetch;      // claim the next read when taking one (GB_FMI_PREFETCH, default off)
   int32_t flags;         // GB_FMI_FLAGS probe switches: 4 = phase clocks into g_fmi_prof,
@@ -288,8 +288,12 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       // would hold its wave, and at the end of the grid the whole step, for its full length: drop
       // what it did (its calls are not counted, a big slot it took is released) and hand it to
       // smem_heavy, which spreads each backward step's independent extensions over a wave
+      // (a big slot it took goes with it: smem_heavy promotes the read into that same slot, so a
+      // handed-over read never holds two of the kMaxOvf slots)
       if (kb_cur >= 0) A.ovf_list[kb_cur] = -1;
-      A.heavy[atomicAdd(A.heavy_n, 1)] = rd;
+      const int h = atomicAdd(A.heavy_n, 1);
+      A.heavy[2 * h] = rd;
+      A.heavy[2 * h + 1] = kb_cur;
       pend = false;
       st = NEXT_READ;
     }
@@ -700,7 +704,8 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
   const int lane = threadIdx.x;
   const int nh = *(volatile const int32_t *)A.heavy_n;
   for (int t = blockIdx.x; t < nh; t += gridDim.x) {
-    const int rd = A.heavy[t];
+    const int rd = A.heavy[2 * t];
+    const int kb_pre = A.heavy[2 * t + 1];  // the big slot the lane kernel had promoted it to, or -1
     const int L = A.lens[rd];
     const int64_t t_read = A.trace ? (int64_t)wall_clock64() : 0;
     for (int i = lane; i < L; i += 64) Q[i] = A.qdb[(size_t)rd * A.stride + i];
@@ -713,9 +718,11 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
     // wave-uniform: o, cap and nout are the same in every lane (the reseed loop below reads them)
     auto emit = [&](int64_t k, int64_t l, int64_t s, uint32_t m, uint32_t n) {
       if (nout == cap && cap == kCap) {
-        int kb = 0;
-        if (lane == 0) kb = atomicAdd(A.ovf_n, 1);
-        kb = __shfl(kb, 0);
+        int kb = kb_pre;
+        if (kb < 0) {
+          if (lane == 0) kb = atomicAdd(A.ovf_n, 1);
+          kb = __shfl(kb, 0);
+        }
         if (kb < kMaxOvf) {
           gb_smem *big = A.big + (size_t)kb * kBigCap;
           if (lane == 0) {
@@ -1035,6 +1042,14 @@ int gb_fmi_debug_trace(gb_fmi_reads *R, int64_t *out) {
   return GB_OK;
 }
 
+int gb_fmi_debug_ctl(gb_fmi_reads *R, int32_t out[8]) {
+  GB_ARG(R && out && R->ran, "gb_fmi_debug_ctl: bad arguments");
+  GB_HIP(hipSetDevice(R->idx->device));
+  GB_HIP(hipStreamSynchronize(R->stream));
+  GB_HIP(hipMemcpy(out, R->d_ctl, 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return GB_OK;
+}
+
 int gb_fmi_debug_prof(uint64_t out[8], int reset) {
   GB_ARG(out, "gb_fmi_debug_prof: null out");
   GB_HIP(hipDeviceSynchronize());
@@ -1216,7 +1231,7 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   reserve(&R->d_slots, &R->cap_slots, nr * gbfmi::kCap * sizeof(gb_smem));
   reserve(&R->d_ovf_pos, &R->cap_ovf_pos, nr * sizeof(int32_t));
   reserve(&R->d_counts, &R->cap_counts, nr * sizeof(int32_t));
-  reserve(&R->d_heavy, &R->cap_heavy, nr * sizeof(int32_t));
+  reserve(&R->d_heavy, &R->cap_heavy, 2 * nr * sizeof(int32_t));
   reserve(&R->d_phase, &R->cap_phase, nr * 3 * sizeof(int32_t));
   reserve(&R->d_offsets, &R->cap_offsets, (nr + 1) * sizeof(int64_t));
   if (e == hipSuccess)

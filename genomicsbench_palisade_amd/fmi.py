@@ -31,6 +31,7 @@ def _decl():
     L.gb_fmi_reads_create.argtypes = [vp, vp, vp, i32, i32, ctypes.POINTER(vp)]
     L.gb_fmi_reads_destroy.argtypes = [vp]
     L.gb_fmi_search.argtypes = [vp, i32]
+    L.gb_fmi_debug_ctl.argtypes = [vp, vp]
     L.gb_fmi_sync.argtypes = [vp]
     L.gb_fmi_results.argtypes = [vp, i32, vp, i64, vp, vp, vp]
     L.gb_fmi_timing.argtypes = [vp, vp, vp, vp]
@@ -159,6 +160,13 @@ class Reads:
         check(_decl().gb_fmi_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
               "gb_fmi_timing")
         return a.value, b.value, c.value
+
+    def ctl(self):
+        """The last search's control words (gb_fmi_debug_ctl): reads taken, big slots taken, fatal
+        overflows, 0, reads handed to the wave pass."""
+        out = np.zeros(8, np.int32)
+        check(_decl().gb_fmi_debug_ctl(self.h, out.ctypes.data), "gb_fmi_debug_ctl")
+        return out
 
     def sa_run(self, max_occ: int = MAX_OCC, mode: int = SA_PREFETCH):
         """SA coordinates of the last search's SMEMs, on the device (bwamem.cpp:737 for every read)."""

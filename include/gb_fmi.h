@@ -140,6 +140,9 @@ int gb_fmi_debug_prof(uint64_t out[8], int reset);
 /* Diagnostic: after a search run with GB_FMI_FLAGS bit 3 (value 8) set, out[3 r .. 3 r + 2] = the
  * wall clock (100 MHz) at which read r was taken and finished, and its backwardExt calls. */
 int gb_fmi_debug_trace(gb_fmi_reads *R, int64_t *out);
+/* Diagnostic: the last search's control words -- out = {reads taken, big (kBigCap) slots taken,
+ * reads past every slot (fatal), 0, reads handed to the wave pass, 0, 0, 0}. */
+int gb_fmi_debug_ctl(gb_fmi_reads *R, int32_t out[8]);
 
 /* Diagnostic, host only (no device work): round trips through the search's packed layouts, the
  * code the kernels run. ent: n entries of {k, l, s, m, n} (k, l, s < 2^34; m, n < 2^13) packed into

@@ -10,6 +10,8 @@ import fmi_util
 from conftest import GOLDEN
 from genomicsbench_palisade_amd import gen
 
+KCAP = 40  # csrc/fmi.hip kCap: first-pass SMEM slots per read
+
 pytestmark = pytest.mark.gpu
 
 
@@ -146,6 +148,13 @@ def test_heavy_read_pass_exact(fmi, monkeypatch, budget, min_seed, rep):
     assert (bc == ebc).all() and (pc == epc).all()
     assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
     assert rs.timing()[2] == oi.bwt_calls()
+    # every read holds at most one big slot, even one promoted by the lane kernel and then handed
+    # over (smem_heavy promotes it into the slot it released)
+    ctl = rs.ctl()
+    per_read = np.bincount(sm["rid"].astype(np.int64), minlength=len(lens))
+    assert ctl[1] == int((per_read > KCAP).sum())
+    if budget in ("1", "60", "150"):
+        assert ctl[4] > 0
 
 
 def test_cli_dropin(fmi, golden, tmp_path):

@@ -17,7 +17,7 @@ import os
 import sys
 
 HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
-       "smem_search": "smem_search", "chain_kernel": "chain_kernel", "chain_rows": "chain_rows", "bsw_extend_kernel": "bsw_extend_kernel",
+       "smem_search": "smem_search", "chain_kernel": "chain_kernel", "chain_rows": "chain_rows", "verify_lanes": "verify_lanes", "bsw_extend_kernel": "bsw_extend_kernel",
        "bsw_lane_kernel": "bsw_lane_kernel", "sa_walk": "sa_walk"}
 
 FETCH_FACTOR = {"gather": 1.0, "stream": 2.0}
@@ -32,6 +32,7 @@ KERNEL_CLASS = {
     "phmm_forward<double>": "stream",
     "chain_kernel": "stream",           # anchors in 64-anchor coalesced blocks
     "chain_rows": "stream",             # anchors staged in 32-anchor coalesced blocks per half
+    "verify_lanes": "stream",           # one split anchor per lane, contiguous anchors per wave
 }
 
 
