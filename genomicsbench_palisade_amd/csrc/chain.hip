@@ -516,14 +516,14 @@ int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool s
   A.prof = prof ? B->d_prof : nullptr;
   A.exp = getenv("GB_CHAIN_EXP") ? atoi(getenv("GB_CHAIN_EXP")) : 0;
   const dim3 g((unsigned)nvc), b(128);
-  static bool attr = false;
-  if (!attr) {
-    for (const void *f : {(const void *)chain_kernel<0, kRingSmall>, (const void *)chain_kernel<1, kRingSmall>,
-                          (const void *)chain_kernel<2, kRingSmall>, (const void *)chain_kernel<0, kRing>,
-                          (const void *)chain_kernel<1, kRing>, (const void *)chain_kernel<2, kRing>})
-      GB_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    attr = true;
-  }
+  if (int st = once_per_device(1, [](const DevLimits &L) -> int {
+        for (const void *f : {(const void *)chain_kernel<0, kRingSmall>, (const void *)chain_kernel<1, kRingSmall>,
+                              (const void *)chain_kernel<2, kRingSmall>, (const void *)chain_kernel<0, kRing>,
+                              (const void *)chain_kernel<1, kRing>, (const void *)chain_kernel<2, kRing>})
+          GB_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.max_dyn));
+        return GB_OK;
+      }))
+    return st;
   const size_t lds_small = sizeof(uint32_t) * (kRingSmall + 64) + sizeof(Slot) * kSlots + 16;
   const size_t lds_full = sizeof(uint32_t) * (kRing + 64) + sizeof(Slot) * kSlots + 16;
   const size_t dyn = spread_lds(nvc, 2, small ? lds_small : lds_full);

@@ -36,10 +36,18 @@ static void ensure_device() {
 
 namespace {
 
-// grow-only page-locked buffer
+// grow-only page-locked buffer, kept per calling thread across calls (the reference's loop calls
+// host_chain_kernel once per input batch) and freed when the thread ends (thread-storage objects of
+// the main thread are destroyed before the HIP runtime's statics)
 struct Pinned {
   void *p = nullptr;
   size_t cap = 0;
+  Pinned() = default;
+  Pinned(const Pinned &) = delete;
+  Pinned &operator=(const Pinned &) = delete;
+  ~Pinned() {
+    if (p) gb_host_free(p);
+  }
   template <typename T>
   T *get(size_t n) {
     const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);

@@ -104,4 +104,14 @@ int launch_rows(gb_chain_batch *B, const VCall *d_vc, int nvc, hipStream_t strea
 // LDS each) over every SIMD: a launch with fewer waves than SIMD slots is latency-bound, and the
 // dispatcher otherwise stacks its workgroups on few CUs. 0 when the launch fills the chip anyway.
 size_t spread_lds(int nwg, int waves_per_wg, size_t static_lds);
+// The current device's CU count and LDS per CU (queried once per device, thread-safe), and the
+// dynamic LDS the chain kernels may request on it (96 KB, less on a device with less LDS).
+struct DevLimits {
+  int cus = 256;
+  size_t lds_per_cu = 160 * 1024;
+  size_t max_dyn = 96 * 1024;
+};
+const DevLimits &dev_limits();
+// Runs set() once per (current device, slot), e.g. hipFuncSetAttribute for a kernel; thread-safe.
+int once_per_device(int slot, int (*set)(const DevLimits &));
 }  // namespace gbchain

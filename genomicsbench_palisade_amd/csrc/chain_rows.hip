@@ -31,6 +31,9 @@
 
 #include <algorithm>
 #include <climits>
+#include <mutex>
+#include <set>
+#include <utility>
 #include <cstdlib>
 #include <cstdint>
 
@@ -397,11 +400,11 @@ int launch_rows(gb_chain_batch *B, const VCall *d_vc, int nvc, hipStream_t strea
   const char *pe = getenv("GB_CHAIN_PRIO");
   A.prio_n = (pe && pe[0] == '0') ? 0 : B->vc.empty() ? 0 : B->vc[0].n;
   const int nwg = (nvc + 1) / 2;
-  static bool attr = false;
-  if (!attr) {
-    GB_HIP(hipFuncSetAttribute((const void *)chain_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    attr = true;
-  }
+  if (int st = once_per_device(0, [](const DevLimits &L) -> int {
+        GB_HIP(hipFuncSetAttribute((const void *)chain_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.max_dyn));
+        return GB_OK;
+      }))
+    return st;
   hipLaunchKernelGGL(chain_rows, dim3((unsigned)nwg), dim3(64), spread_lds(nwg, 1, sizeof(uint32_t) * (2 * kHalfWords + 64)),
                      stream, A);
   GB_HIP(hipGetLastError());
@@ -411,20 +414,52 @@ int launch_rows(gb_chain_batch *B, const VCall *d_vc, int nvc, hipStream_t strea
 size_t spread_lds(int nwg, int waves_per_wg, size_t static_lds) {
   const char *e = getenv("GB_CHAIN_SPREAD");
   if (e && e[0] == '0') return 0;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
-                                                                                                   : 256;
-  }
+  const DevLimits &L = dev_limits();
   // waves per SIMD one round needs, then the workgroups per CU that gives
   const int64_t waves = (int64_t)nwg * waves_per_wg;
-  const int64_t per_simd = std::max<int64_t>(1, (waves + 4ll * cus - 1) / (4ll * cus));
+  const int64_t per_simd = std::max<int64_t>(1, (waves + 4ll * L.cus - 1) / (4ll * L.cus));
   const int64_t wg_per_cu = std::max<int64_t>(1, per_simd * 4 / waves_per_wg);
-  const size_t budget = (size_t)(160 * 1024 / wg_per_cu);
+  const size_t budget = L.lds_per_cu / (size_t)wg_per_cu;
   if (budget <= static_lds + 1024) return 0;
-  return std::min<size_t>(budget - static_lds - 512, 96 * 1024);
+  return std::min<size_t>(budget - static_lds - 512, L.max_dyn);
+}
+
+namespace {
+constexpr int kMaxDevices = 64;
+std::once_flag g_lim_once[kMaxDevices];
+DevLimits g_lim[kMaxDevices];
+std::mutex g_attr_mu;
+std::set<std::pair<int, int>> g_attr_done;
+
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  return std::min(std::max(dev, 0), kMaxDevices - 1);
+}
+}  // namespace
+
+const DevLimits &dev_limits() {
+  const int dev = current_device();
+  std::call_once(g_lim_once[dev], [dev] {
+    DevLimits L;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+      if (prop.multiProcessorCount > 0) L.cus = prop.multiProcessorCount;
+      if (prop.maxSharedMemoryPerMultiProcessor > 0) L.lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
+    }
+    L.max_dyn = L.lds_per_cu > 64 * 1024 ? std::min<size_t>(96 * 1024, L.lds_per_cu - 32 * 1024) : L.lds_per_cu / 2;
+    g_lim[dev] = L;
+  });
+  return g_lim[dev];
+}
+
+int once_per_device(int slot, int (*set)(const DevLimits &)) {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lk(g_attr_mu);
+  if (g_attr_done.count({dev, slot})) return GB_OK;
+  if (int st = set(dev_limits())) return st;
+  g_attr_done.insert({dev, slot});
+  return GB_OK;
 }
 
 }  // namespace gbchain

@@ -200,6 +200,21 @@ int64_t FMI_search::bwtSeedStrategyAllPosOneThread(uint8_t *enc_qdb, int32_t *ma
   return n;
 }
 
+// getSMEMs (FMI_search.cpp:1328-1497): matchArray from its start, numTotalSmem[0] = the count (the
+// reference's commented-out OpenMP region leaves the other entries untouched); batch_size is unused
+// there too
+void FMI_search::getSMEMs(uint8_t *enc_qdb, int32_t numReads, int32_t batch_size, int32_t readlength,
+                          int32_t minSeedLen, int32_t nthreads, SMEM *matchArray, int64_t *numTotalSmem) {
+  (void)batch_size;
+  ensure_device(device_);
+  int64_t n = 0, calls = 0;
+  const int st = gb_fmi_get_smems(idx_, enc_qdb, numReads, readlength, minSeedLen, nthreads,
+                                  reinterpret_cast<gb_smem *>(matchArray), INT64_MAX, &n, &calls);
+  if (st) die("getSMEMs", st);
+  static_cast<Lock *>(lock_)->calls += calls;
+  numTotalSmem[0] = n;
+}
+
 // sortSMEMs (FMI_search.cpp:1520-1534): per "thread" segment starting at first * readlength, a sort by
 // compare_smem; glibc's qsort is a stable merge sort, so ties keep their order here too.
 void FMI_search::sortSMEMs(SMEM *matchArray, int64_t numTotalSmem[], int32_t numReads, int32_t readlength,

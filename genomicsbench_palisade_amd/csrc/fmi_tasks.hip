@@ -6,6 +6,8 @@
 //   getSMEMsOnePosOneThread          FMI_search.cpp:986-1180   task = (rid, x, min_intv)
 //   getSMEMsAllPosOneThread          FMI_search.cpp:1182-1241  task = (rid, min_intv), every x start
 //   bwtSeedStrategyAllPosOneThread   FMI_search.cpp:1243-1326  task = (read i, max_intv)
+//   getSMEMs                         FMI_search.cpp:1328-1497  task = read i (right-to-left search
+//                                    over fixed-stride reads; no caller in the benchmarks)
 // and expects the matchArray in the reference's emission order. One task per lane: the lane runs the
 // reference loop for its task (backwardExt over the same Occ32 blocks as the fused kernel, `prev` list
 // in a private global scratch row) and appends (SMEM, round) records to its slot; the host adapter
@@ -16,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <cstdlib>
@@ -30,7 +33,7 @@
 namespace gbfmi {
 namespace {
 
-enum TaskMode { kOnePos = 0, kAllPos = 1, kLast = 2 };
+enum TaskMode { kOnePos = 0, kAllPos = 1, kLast = 2, kRight = 3 };
 
 struct TSmem {  // gb_smem with the round in the padding word
   uint32_t rid, m, n, round;
@@ -55,7 +58,7 @@ struct TaskArgs {
   int32_t *counts;             // per task: records emitted (may exceed cap)
   int16_t *next_pos;           // per task (OnePos)
   int32_t *rounds;             // per task (AllPos)
-  TEnt *prev;                  // per task: maxlen + 1 entries
+  TEnt *prev;                  // per task: maxlen + 2 entries
   unsigned long long *calls;   // backwardExt calls (work counter)
 };
 
@@ -99,7 +102,7 @@ __device__ int one_pos(const TaskArgs &A, int t, uint32_t rid, int x, int32_t mi
   const DevIndex &F = A.F;
   const uint8_t *q = A.qdb + A.offs[rid];
   const int len = A.lens[rid];
-  TEnt *prev = A.prev + (size_t)t * (A.maxlen + 1);
+  TEnt *prev = A.prev + (size_t)t * (A.maxlen + 2);
   int next_x = x + 1;
   int a = q[x];
   if (a >= 4) return next_x;
@@ -198,6 +201,83 @@ __device__ void last_seeds(const TaskArgs &A, int t, uint32_t i, int32_t max_int
   }
 }
 
+// getSMEMs for read i (FMI_search.cpp:1328-1497), with the reference's own behaviour: SMEMs are found
+// right to left (forward extension from x, then backward from x - 1); a forward extension stopped by
+// an ambiguous base pushes the current SMEM twice (:1394-1401); the aliased prev/curr arrays
+// (:1345-1346) are in-place compaction, as here. Emits in the reference's order.
+__device__ void right_smems(const TaskArgs &A, int t, uint32_t i, int &cnt, unsigned &calls) {
+  const DevIndex &F = A.F;
+  const uint8_t *q = A.qdb + A.offs[i];
+  const int len = A.lens[i];
+  TEnt *prev = A.prev + (size_t)t * (A.maxlen + 2);
+  int x = len - 1, numPrev = 0;
+  while (x >= 0) {
+    int a = q[x];
+    if (a > 3) {
+      x--;
+      continue;
+    }
+    TEnt sm;
+    sm.m = sm.n = (uint32_t)x;
+    sm.k = count_of(F, a);
+    sm.l = count_of(F, 3 - a);
+    sm.s = count_of(F, a + 1) - count_of(F, a);
+    for (int j = x + 1; j < len; j++) {
+      a = q[j];
+      if (a < 4) {
+        TEnt ns = fwd_ext(F, sm, a, calls);
+        ns.n = (uint32_t)j;
+        if (ns.s != sm.s) prev[numPrev++] = sm;
+        sm = ns;
+        if (ns.s == 0) break;
+      } else {
+        prev[numPrev++] = sm;
+        break;
+      }
+    }
+    if (sm.s != 0) prev[numPrev++] = sm;
+    for (int p = 0; p < numPrev / 2; p++) {
+      const TEnt tmp = prev[p];
+      prev[p] = prev[numPrev - p - 1];
+      prev[numPrev - p - 1] = tmp;
+    }
+    int next_x = x - 1, cur_j = len;
+    for (int j = x - 1; j >= 0; j--) {
+      int numCurr = 0;
+      int curr_s = -1;  // int in the reference
+      a = q[j];
+      if (a > 3) {
+        next_x = j - 1;
+        break;
+      }
+      for (int p = 0; p < numPrev; p++) {
+        const TEnt s0 = prev[p];
+        TEnt ns = bwd_ext(F, s0, a, calls);
+        ns.m = (uint32_t)j;
+        if (ns.s == 0 && numCurr == 0 && j < cur_j) {
+          cur_j = j;
+          if ((s0.n - s0.m + 1) >= (uint32_t)A.min_seed_len) emit(A, t, cnt, i, s0, 0);
+        }
+        if (ns.s != 0 && ns.s != (int64_t)curr_s) {
+          curr_s = (int)ns.s;
+          prev[numCurr++] = ns;
+        }
+      }
+      numPrev = numCurr;
+      if (numCurr == 0) {
+        next_x = j;
+        break;
+      }
+      next_x = j - 1;
+    }
+    if (numPrev != 0) {
+      if ((prev[0].n - prev[0].m + 1) >= (uint32_t)A.min_seed_len) emit(A, t, cnt, i, prev[0], 0);
+      numPrev = 0;
+    }
+    x = next_x;
+  }
+}
+
 template <int kMode>
 __global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,8 +296,10 @@ __global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
         round++;
       }
       A.rounds[t] = (int32_t)round;
-    } else {
+    } else if (kMode == kLast) {
       last_seeds(A, t, rid, A.intv[t], cnt, calls);
+    } else {
+      right_smems(A, t, rid, cnt, calls);
     }
     A.counts[t] = cnt;
   }
@@ -325,7 +407,10 @@ struct HostTasks {
 int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *lens, const int32_t *offs, int32_t nrid,
               const HostTasks &T, int32_t min_seed_len, std::vector<std::vector<TSmem>> &recs,
               std::vector<int16_t> *next_pos, std::vector<int32_t> *rounds, int64_t *calls_out) {
-  gb::Range range_(mode == kOnePos ? "gb.fmi.onepos" : mode == kAllPos ? "gb.fmi.allpos" : "gb.fmi.last");
+  gb::Range range_(mode == kOnePos ? "gb.fmi.onepos"
+                   : mode == kAllPos ? "gb.fmi.allpos"
+                   : mode == kLast   ? "gb.fmi.last"
+                                     : "gb.fmi.get_smems");
   const int32_t ntasks = (int32_t)T.rid.size();
   recs.assign(ntasks, {});
   if (next_pos) next_pos->assign(ntasks, 0);
@@ -338,7 +423,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   for (int32_t t = 0; t < ntasks; t++) {
     const int32_t r = T.rid[t];
     GB_ARG(r >= 0 && r < nrid, "FMI_search: task %d names read %d outside [0, %d)", t, r, nrid);
-    GB_ARG(lens[r] >= 0 && lens[r] < 32768 && offs[r] >= 0, "FMI_search: read %d has length %d / offset %d", r,
+    GB_ARG(lens[r] >= 0 && (lens[r] < 32768 || mode == kRight) && offs[r] >= 0, "FMI_search: read %d has length %d / offset %d", r,
            lens[r], offs[r]);
     if (mode == kOnePos)
       GB_ARG(T.qpos[t] >= 0 && T.qpos[t] < lens[r], "FMI_search: query position %d outside read %d (length %d)",
@@ -361,7 +446,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   // Tiles of at most ~256 MB of `prev` scratch ((maxlen + 1) entries per task): the per-thread
   // workspace stays bounded whatever the batch. Per tile: the whole tile, then its overflowing
   // subset with a slot sized to its largest count.
-  int64_t tile = std::max<int64_t>(64, ((256ll << 20) / ((int64_t)(maxlen + 1) * (int64_t)sizeof(TEnt))) & ~63ll);
+  int64_t tile = std::max<int64_t>(64, ((256ll << 20) / ((int64_t)(maxlen + 2) * (int64_t)sizeof(TEnt))) & ~63ll);
   if (const char *te = getenv("GB_FMI_TASK_TILE")) tile = std::max(1, atoi(te));  // tests: force many tiles
   bool uploaded = false;
   int64_t calls_sum = 0;
@@ -369,7 +454,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   const int32_t t1 = (int32_t)std::min<int64_t>(ntasks, t0 + tile);
   std::vector<int32_t> todo(t1 - t0);
   for (int32_t t = t0; t < t1; t++) todo[t - t0] = t;
-  int32_t cap = mode == kLast ? 48 : 32;
+  int32_t cap = mode == kLast ? 48 : mode == kRight ? 64 : 32;
   for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
     const int32_t n = (int32_t)todo.size();
     std::vector<int32_t> rid(n), intv(n);
@@ -387,7 +472,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     if (e == hipSuccess) e = W.ensure(5, sizeof(int32_t) * (size_t)n);
     if (e == hipSuccess) e = W.ensure(6, sizeof(TSmem) * (size_t)n * cap);
     if (e == hipSuccess) e = W.ensure(7, sizeof(int32_t) * 2 * (size_t)n + sizeof(int16_t) * (size_t)n + 64);
-    if (e == hipSuccess) e = W.ensure(8, sizeof(TEnt) * (size_t)n * (maxlen + 1));
+    if (e == hipSuccess) e = W.ensure(8, sizeof(TEnt) * (size_t)n * (maxlen + 2));
     if (e == hipSuccess) e = W.ensure(9, sizeof(unsigned long long));
     GB_HIP(e);
     A.qdb = (const uint8_t *)W.buf[0];
@@ -417,7 +502,7 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
     GB_HIP(hipMemcpyAsync(W.buf[5], intv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     // a wave per task when the reads fit its LDS lists (GB_FMI_TASK_WAVE=0: a lane per task)
     const char *we = getenv("GB_FMI_TASK_WAVE");
-    if (maxlen <= kWaveMaxLen && !(we && *we == '0')) {
+    if (mode != kRight && maxlen <= kWaveMaxLen && !(we && *we == '0')) {
       const dim3 grid((unsigned)std::min<int64_t>(n, 65535)), block(64);
       if (mode == kOnePos)
         hipLaunchKernelGGL(fmi_task_wave<kOnePos>, grid, block, 0, s, A);
@@ -431,8 +516,10 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
         hipLaunchKernelGGL(fmi_task_kernel<kOnePos>, grid, block, 0, s, A);
       else if (mode == kAllPos)
         hipLaunchKernelGGL(fmi_task_kernel<kAllPos>, grid, block, 0, s, A);
-      else
+      else if (mode == kLast)
         hipLaunchKernelGGL(fmi_task_kernel<kLast>, grid, block, 0, s, A);
+      else
+        hipLaunchKernelGGL(fmi_task_kernel<kRight>, grid, block, 0, s, A);
     }
     GB_HIP(hipGetLastError());
     std::vector<int32_t> ctl(2 * (size_t)n);
@@ -613,6 +700,40 @@ int gb_fmi_last_seeds(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *
   *nout = tot;
   if (!out) return GB_OK;
   GB_ARG(tot <= out_cap, "gb_fmi_last_seeds: %lld SMEMs exceed out_cap %lld", (long long)tot, (long long)out_cap);
+  int64_t o = 0;
+  for (auto &v : recs)
+    for (auto &r : v) put(out + o++, r);
+  return GB_OK;
+}
+
+int gb_fmi_get_smems(gb_fmi_index *idx, const uint8_t *enc_qdb, int32_t num_reads, int32_t readlength,
+                     int32_t min_seed_len, int32_t nthreads, gb_smem *out, int64_t out_cap, int64_t *nout,
+                     int64_t *bwt_calls) {
+  GB_ARG(idx && nout && num_reads >= 0 && readlength >= 0 && nthreads >= 1, "gb_fmi_get_smems: bad arguments");
+  GB_ARG(num_reads == 0 || readlength == 0 || enc_qdb, "gb_fmi_get_smems: null enc_qdb");
+  // the reference's omp region is commented out (tid 0): only the first thread's quota of reads
+  const int32_t last = std::min<int64_t>(num_reads, ((int64_t)num_reads + nthreads - 1) / nthreads);
+  *nout = 0;
+  if (bwt_calls) *bwt_calls = 0;
+  if (last == 0 || readlength == 0) return GB_OK;
+  GB_ARG((int64_t)last * readlength < INT32_MAX, "gb_fmi_get_smems: %d reads x %d bases exceed 2^31", last, readlength);
+  HostTasks T;
+  T.rid.resize(last);
+  T.intv.assign(last, 0);
+  std::vector<int32_t> lens(last, readlength), offs(last);
+  for (int32_t i = 0; i < last; i++) {
+    T.rid[i] = i;
+    offs[i] = (int32_t)((int64_t)i * readlength);
+  }
+  std::vector<std::vector<TSmem>> recs;
+  int st = run_tasks(idx, kRight, enc_qdb, lens.data(), offs.data(), last, T, min_seed_len, recs, nullptr, nullptr,
+                     bwt_calls);
+  if (st) return st;
+  int64_t tot = 0;
+  for (auto &v : recs) tot += (int64_t)v.size();
+  *nout = tot;
+  if (!out) return GB_OK;
+  GB_ARG(tot <= out_cap, "gb_fmi_get_smems: %lld SMEMs exceed out_cap %lld", (long long)tot, (long long)out_cap);
   int64_t o = 0;
   for (auto &v : recs)
     for (auto &r : v) put(out + o++, r);

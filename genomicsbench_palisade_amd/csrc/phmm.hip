@@ -41,9 +41,12 @@
 namespace {
 
 constexpr int kWave = 64;
-// Longest haplotype: the f64 kernel's LDS (16-B boundary record + 1 code byte per column, plus
-// kBndPad + kWave pad columns) must fit the 160 KB of one CU.
-constexpr int kMaxHaplen = 9400;
+// Longest haplotype a stack keeps in LDS: the f64 kernel's LDS (16-B boundary record + 1 code byte
+// per column, plus kBndPad + kWave pad columns) must fit the 160 KB of one CU. Stacks of longer
+// haplotypes (up to kMaxHaplen, the 16-bit field of TcDesc::dims) keep the same records in a global
+// scratch area per workgroup instead (phmm_forward<.., kLong>): the reference GKL has no cap.
+constexpr int kLdsHaplen = 9400;
+constexpr int kMaxHaplen = 65535;
 constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_stripe reads)
 constexpr int kRecPad = 4;   // boundary records below column 0 (lane 63's writes start at column -2)
 constexpr int kQualTab = 128;
@@ -366,7 +369,7 @@ __device__ __forceinline__ int scan_add(int v) {  // wave-wide inclusive prefix 
 // One stack. f32 pass: every testcase; f64 pass: those whose f32 result is below MIN_ACCEPTED
 // (all of them when `force`). Returns the number of testcases computed.
 template <typename T, bool kF64Pass>
-__device__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
+__device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
                           const uint8_t *__restrict__ pool, const DevTab<T> &tab, T *__restrict__ raw_out,
                           const float *__restrict__ raw_f, bool force, uint8_t *smem_raw) {
   const int lane = threadIdx.x;
@@ -496,27 +499,34 @@ __device__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, c
 // f32 pass: one stack per workgroup (LPT order). f64 pass: a persistent grid takes stacks through
 // counter[1] and recomputes their testcases whose f32 result fell below MIN_ACCEPTED; counter[0]
 // counts them.
-template <typename T, bool kF64Pass>
+// kLong: stacks whose haplotype is longer than kLdsHaplen; their boundary records and codes live in
+// `scratch` (scratch_stride bytes per workgroup, global memory: lane 63's record stores and lane 0's
+// loads of the next stripe are ordered by the stripe's __syncthreads), and both passes take the
+// stacks through a persistent grid (counter[2] f32, counter[3] f64).
+template <typename T, bool kF64Pass, bool kLong = false>
 __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ stacks, int nstacks,
                                                     const uint32_t *__restrict__ stk_tc,
                                                     const TcDesc *__restrict__ descs,
                                                     const uint8_t *__restrict__ pool, DevTab<T> tab,
                                                     T *__restrict__ raw_out, const float *__restrict__ raw_f,
-                                                    int *__restrict__ counter, int force) {
+                                                    int *__restrict__ counter, int force, uint8_t *scratch,
+                                                    size_t scratch_stride) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-  if constexpr (kF64Pass) {
+  uint8_t *rec = kLong ? scratch + (size_t)blockIdx.x * scratch_stride : smem_raw;
+  if constexpr (kF64Pass || kLong) {
     int done = 0;
+    int *next = counter + (kLong ? (kF64Pass ? 3 : 2) : 1);
     while (true) {
       int k = 0;
-      if (threadIdx.x == 0) k = atomicAdd(counter + 1, 1);
+      if (threadIdx.x == 0) k = atomicAdd(next, 1);
       k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
       if (k >= nstacks) break;
-      done += phmm_stack<T, true>(stacks[k], stk_tc, descs, pool, tab, raw_out, raw_f, force != 0, smem_raw);
-      __syncthreads();  // the next stack re-initialises the LDS
+      done += phmm_stack<T, kF64Pass>(stacks[k], stk_tc, descs, pool, tab, raw_out, raw_f, force != 0, rec);
+      __syncthreads();  // the next stack re-initialises the records
     }
-    if (threadIdx.x == 0 && done) atomicAdd(counter, done);
+    if (kF64Pass && threadIdx.x == 0 && done) atomicAdd(counter, done);
   } else {
-    phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, smem_raw);
+    phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec);
   }
 }
 
@@ -647,8 +657,13 @@ struct gb_phmm_batch {
   double *d_out = nullptr;
   uint32_t *d_stk_tc = nullptr;  // testcase indices, stack by stack
   Stack *d_stacks = nullptr;     // LPT order
-  int nstacks = 0;
-  int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter
+  int nstacks = 0;                 // stacks whose haplotype fits the LDS (the first nstacks)
+  int n_long = 0;                  // stacks behind them whose haplotype does not (kLong kernels)
+  int long_grid = 0;               // their persistent grid
+  uint8_t *d_scratch = nullptr;    // their boundary records, scratch_stride bytes per workgroup
+  size_t scratch_stride = 0, cap_scratch = 0;
+  int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter,
+                           // [2] / [3] the kLong f32 / f64 stack counters
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
   int cus = 256;                   // compute units of the device (stack height rule)
@@ -871,15 +886,27 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     stacks.push_back(S);
     scost.push_back((uint64_t)((rows + kWave - 1) / kWave) * (uint64_t)(C + kWave));
   }
-  // stable counting sort by decreasing cost (at most 1026 stripes x (kMaxHaplen + 64) columns)
+  // by decreasing cost (stable), the stacks whose haplotype does not fit the LDS behind the others
+  // (they run on the kLong kernels)
   std::vector<Stack> sorted_stacks(stacks.size());
+  int n_long = 0, max_h_short = 0, max_h_long = 0;
   {
-    uint64_t cmax = 0;
-    for (uint64_t c : scost) cmax = std::max(cmax, c);
-    std::vector<uint32_t> at((size_t)cmax + 2, 0);
-    for (uint64_t c : scost) at[(size_t)(cmax - c) + 1]++;
-    for (size_t c = 1; c < at.size(); c++) at[c] += at[c - 1];
-    for (size_t k = 0; k < stacks.size(); k++) sorted_stacks[at[(size_t)(cmax - scost[k])]++] = stacks[k];
+    std::vector<uint32_t> idx(stacks.size());
+    for (size_t k = 0; k < idx.size(); k++) {
+      idx[k] = (uint32_t)k;
+      const int C = (int)stacks[k].C;
+      if (C > kLdsHaplen) {
+        n_long++;
+        max_h_long = std::max(max_h_long, C);
+      } else {
+        max_h_short = std::max(max_h_short, C);
+      }
+    }
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      const bool la = stacks[a].C > (uint32_t)kLdsHaplen, lb = stacks[b].C > (uint32_t)kLdsHaplen;
+      return la != lb ? lb : scost[a] > scost[b];
+    });
+    for (size_t k = 0; k < idx.size(); k++) sorted_stacks[k] = stacks[idx[k]];
   }
   std::vector<uint32_t> stk_tc(order.begin(), order.end());
   if (pool.empty()) pool.resize(4);
@@ -912,7 +939,21 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     GB_HIP(hipMalloc(&b->d_pool, pool.size()));
     b->cap_pool = pool.size();
   }
-  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 2 * sizeof(int)));
+  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 4 * sizeof(int)));
+  if (n_long) {
+    // records + codes of one long stack per workgroup of the persistent kLong grid
+    b->long_grid = std::min(n_long, b->f64_grid);
+    b->scratch_stride = (sizeof(Brec<double>) * (size_t)(max_h_long + kBndPad + kRecPad) +
+                         (size_t)(max_h_long + kBndPad + kWave) + 16 + 255) & ~(size_t)255;
+    const size_t need = b->scratch_stride * (size_t)b->long_grid;
+    if (need > b->cap_scratch) {
+      (void)hipFree(b->d_scratch);
+      b->d_scratch = nullptr;
+      b->cap_scratch = 0;
+      GB_HIP(hipMalloc(&b->d_scratch, need));
+      b->cap_scratch = need;
+    }
+  }
   if (n) {
     GB_HIP(hipMemcpyAsync(b->d_desc, desc.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
     GB_HIP(hipMemcpyAsync(b->d_stk_tc, stk_tc.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
@@ -923,8 +964,10 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
   clk.mark("upload");
   b->n = n;
-  b->nstacks = (int)sorted_stacks.size();
-  b->max_haplen = max_h;
+  b->nstacks = (int)sorted_stacks.size() - n_long;
+  b->n_long = n_long;
+  b->max_haplen = max_h_short;
+  (void)max_h;
   b->cells = cells;
   b->ran = false;
   return GB_OK;
@@ -993,7 +1036,7 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipSetDevice(t->device));
   const int n = b->n;
   GB_HIP(hipEventRecord(b->ev[0], b->stream));
-  GB_HIP(hipMemsetAsync(b->d_count, 0, 2 * sizeof(int), b->stream));
+  GB_HIP(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
     const size_t rec = (size_t)(b->max_haplen + kBndPad + kRecPad), codes = (size_t)(b->max_haplen + kBndPad + kWave);
@@ -1001,19 +1044,31 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
     const size_t lds_d = sizeof(Brec<double>) * rec + codes + 16;
     auto f32k = phmm_forward<float, false>;
     auto f64k = phmm_forward<double, true>;
-    const int ns = b->nstacks;
+    const int ns = b->nstacks, nl = b->n_long;
+    const Stack *d_long = b->d_stacks + ns;
     if (!b->force_f64) {
-      hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
-                         b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
-                         b->d_count, 0);
+      if (ns > 0)
+        hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
+                           b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
+                           b->d_count, 0, (uint8_t *)nullptr, (size_t)0);
+      if (nl > 0)
+        hipLaunchKernelGGL((phmm_forward<float, false, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
+                           nl, b->d_stk_tc, b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,
+                           (const float *)nullptr, b->d_count, 0, b->d_scratch, b->scratch_stride);
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
     // f64 fallback: persistent grid over the stacks, each recomputing its flagged testcases
-    const int g64 = std::min(ns, b->f64_grid);
-    hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
-                       b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
-                       b->d_count, b->force_f64 ? 1 : 0);
+    if (ns > 0) {
+      const int g64 = std::min(ns, b->f64_grid);
+      hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
+                         b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
+                         b->d_count, b->force_f64 ? 1 : 0, (uint8_t *)nullptr, (size_t)0);
+    }
+    if (nl > 0)
+      hipLaunchKernelGGL((phmm_forward<double, true, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
+                         nl, b->d_stk_tc, b->d_desc, b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
+                         (const float *)b->d_rf, b->d_count, b->force_f64 ? 1 : 0, b->d_scratch, b->scratch_stride);
     GB_HIP(hipGetLastError());
     GB_HIP(hipEventRecord(b->ev[2], b->stream));
     hipLaunchKernelGGL(phmm_finalize, dim3((n + 255) / 256), dim3(256), 0, b->stream, b->d_rf,
@@ -1113,6 +1168,7 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   (void)hipFree(b->d_stk_tc);
   (void)hipFree(b->d_stacks);
   (void)hipFree(b->d_count);
+  (void)hipFree(b->d_scratch);
   for (auto e : b->ev)
     if (e) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamDestroy(b->stream);

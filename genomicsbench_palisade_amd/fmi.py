@@ -32,6 +32,7 @@ def _decl():
     L.gb_fmi_reads_destroy.argtypes = [vp]
     L.gb_fmi_search.argtypes = [vp, i32]
     L.gb_fmi_debug_ctl.argtypes = [vp, vp]
+    L.gb_fmi_get_smems.argtypes = [vp, vp, i32, i32, i32, i32, vp, i64, vp, vp]
     L.gb_fmi_sync.argtypes = [vp]
     L.gb_fmi_results.argtypes = [vp, i32, vp, i64, vp, vp, vp]
     L.gb_fmi_timing.argtypes = [vp, vp, vp, vp]
@@ -106,6 +107,20 @@ class Index:
                                         len(coords), counts.ctypes.data, ctypes.byref(tot)),
               "gb_fmi_sa_entries")
         return coords[:tot.value], counts[:n]
+
+    def get_smems(self, codes: np.ndarray, num_reads: int, min_seed_len: int = 19, nthreads: int = 1):
+        """FMI_search::getSMEMs over fixed-stride reads (codes: num_reads x readlength) -> (SMEMs in the
+        reference's order, backwardExt calls)."""
+        L = _decl()
+        codes = np.ascontiguousarray(codes, np.uint8)
+        rl = codes.shape[1] if codes.ndim == 2 else 0
+        n, calls = ctypes.c_int64(), ctypes.c_int64()
+        check(L.gb_fmi_get_smems(self.h, codes.ctypes.data, num_reads, rl, min_seed_len, nthreads, None, 0,
+                                 ctypes.byref(n), ctypes.byref(calls)), "gb_fmi_get_smems")
+        out = np.zeros(max(n.value, 1), SMEM_DTYPE)
+        check(L.gb_fmi_get_smems(self.h, codes.ctypes.data, num_reads, rl, min_seed_len, nthreads, out.ctypes.data,
+                                 len(out), ctypes.byref(n), ctypes.byref(calls)), "gb_fmi_get_smems")
+        return out[:n.value], calls.value
 
     def close(self):
         if self.h:

@@ -11,14 +11,15 @@
  *   class FMI_search                 tools/bwa-mem2/src/FMI_search.h:101-224, public methods:
  *     FMI_search(fname), ~FMI_search, build_index, load_index            FMI_search.cpp:51-984
  *     getSMEMsOnePosOneThread / getSMEMsAllPosOneThread                  :986-1241
- *     bwtSeedStrategyAllPosOneThread, sortSMEMs                          :1243-1326, :1520-1534
+ *     bwtSeedStrategyAllPosOneThread, getSMEMs, sortSMEMs                :1243-1497, :1520-1534
  *     get_sa_entry, get_sa_entries (x3), get_sa_entry_compressed,        :1566-2040
  *     call_one_step, get_sa_entries_prefetch
  * Implemented by genomicsbench_palisade_amd/lib/libgb_fmi_dropin.so (csrc/fmi_dropin.cpp): the index
  * lives in HBM of the device selected by $GB_DEVICE (default 0) and every SMEM / SA method runs HIP
  * kernels there (csrc/fmi_tasks.hip, csrc/fmi_sa.hip), returning the reference's outputs in the
  * reference's order. One object may be shared by host threads, as fmi.cpp's OpenMP loop does.
- * Not provided: getSMEMs (FMI_search.cpp:1328-1497; fmi.cpp does not call it) and the HE members.
+ * Not provided: the HE members. (getSMEMs, which no benchmark calls, keeps its reference behaviour:
+ * only the first ceil(numReads / nthreads) reads are searched, see gb_fmi_get_smems.)
  */
 #ifndef GB_COMPAT_FMI_SEARCH_H
 #define GB_COMPAT_FMI_SEARCH_H
@@ -69,6 +70,9 @@ class FMI_search {
   int64_t bwtSeedStrategyAllPosOneThread(uint8_t *enc_qdb, int32_t *max_intv_array, int32_t numReads,
                                          const bseq1_t *seq_, int32_t *query_cum_len_ar, int32_t minSeedLen,
                                          SMEM *matchArray);
+
+  void getSMEMs(uint8_t *enc_qdb, int32_t numReads, int32_t batch_size, int32_t readlength, int32_t minSeedLen,
+                int32_t nthreads, SMEM *matchArray, int64_t *numTotalSmem);
 
   void sortSMEMs(SMEM *matchArray, int64_t numTotalSmem[], int32_t numReads, int32_t readlength, int nthreads);
 

@@ -125,6 +125,13 @@ int gb_fmi_smem_allpos(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t 
 int gb_fmi_last_seeds(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t *lens, const int32_t *offs,
                       int32_t nreads, const int32_t *max_intv, int32_t min_seed_len, gb_smem *out, int64_t out_cap,
                       int64_t *nout, int64_t *bwt_calls);
+/* getSMEMs (FMI_search.cpp:1328-1497): right-to-left SMEMs of fixed-stride reads (read i =
+ * enc_qdb[i * readlength ..], every base a position), with the reference's behaviour: its OpenMP region
+ * is commented out, so only reads [0, ceil(num_reads / nthreads)) are searched, and *nout is what it
+ * leaves in numTotalSmem[0]; SMEMs in read order, each read's in emission order (rid = i). */
+int gb_fmi_get_smems(gb_fmi_index *idx, const uint8_t *enc_qdb, int32_t num_reads, int32_t readlength,
+                     int32_t min_seed_len, int32_t nthreads, gb_smem *out, int64_t out_cap, int64_t *nout,
+                     int64_t *bwt_calls);
 
 /* get_sa_entry / get_sa_entries(pos[]) (FMI_search.cpp:1566-1586): the raw sampled-SA entries at
  * indices pos[i] (0 <= pos < (n >> 3) + 1, sa_ms_byte << 32 + sa_ls_word). */

@@ -40,10 +40,12 @@ typedef struct gb_testcase {
 /* initPairHMM(): builds the probability tables (Context.h) on the host and uploads them. */
 int gb_phmm_init(void);
 
-/* Limits: 1 <= rslen <= 65535 and 1 <= haplen <= 9400 (the f64 pass keeps one haplotype's boundary
- * records and codes, 17 bytes per column, in the 160 KB of LDS of one CU); a testcase outside them
- * fails the call with GB_ERR_ARG before any device work (the reference GKL kernels have no haplotype
- * cap; the GKL-named drop-in aborts on such input).
+/* Limits: 1 <= rslen <= 65535 and 1 <= haplen <= 65535 (the 16-bit fields of the packed testcase
+ * descriptor). Haplotypes up to 9400 bases keep a stack's boundary records and codes (17 bytes per
+ * column) in one CU's LDS; longer ones run on kernels that keep them in a global scratch area per
+ * workgroup, with the same arithmetic. A testcase outside the limits fails the call with GB_ERR_ARG
+ * before any device work (the reference GKL kernels have no cap; the GKL-named drop-in aborts on such
+ * input).
  *
  * computelikelihoodsboth(): results[k] = log10-likelihood of tcs[k], bit-identical to the
  * reference. raw_f / raw_d / used_double may be NULL; when given they receive the raw f32

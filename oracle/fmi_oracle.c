@@ -556,6 +556,93 @@ int64_t fmi_oracle_phase(or_fmi *f, int phase, const uint8_t *qdb, const int32_t
   return nt;
 }
 
+/* FMI_search::getSMEMs, FMI_search.cpp:1328-1497: right-to-left SMEMs over fixed-stride reads.
+ * Restated with the reference's quirks, which are its behaviour: the OpenMP region is commented out
+ * (tid = 0), so only the first ceil(numReads / nthreads) reads are searched and only numTotalSmem[0]
+ * is written; myPrevArray and myCurrArray are the same buffer (:1345-1346), which the backward loop
+ * uses as in-place compaction (a write never overtakes the entry being read); a forward extension
+ * stopped by an N pushes the current SMEM twice (:1394-1401). prev needs readlength + 2 entries. */
+void fmi_oracle_get_smems(or_fmi *f, const uint8_t *enc_qdb, int32_t numReads, int32_t readlength,
+                          int32_t minSeedLen, int32_t nthreads, or_smem *matchArray, int64_t *numTotalSmem) {
+  or_smem *prev = (or_smem *)malloc((size_t)(readlength + 2) * sizeof(or_smem));
+  numTotalSmem[0] = 0;
+  int32_t quota = (numReads + (nthreads - 1)) / nthreads;
+  int32_t last = quota > numReads ? numReads : quota;
+  for (int32_t i = 0; i < last; i++) {
+    const uint8_t *q = enc_qdb + (int64_t)i * readlength;
+    int x = readlength - 1, numPrev = 0, numSmem = 0;
+    while (x >= 0) {
+      uint8_t a = q[x];
+      if (a > 3) {
+        x--;
+        continue;
+      }
+      or_smem smem;
+      smem.rid = (uint32_t)i;
+      smem.m = smem.n = (uint32_t)x;
+      smem.k = f->count[a];
+      smem.l = f->count[3 - a];
+      smem.s = f->count[a + 1] - f->count[a];
+      int j;
+      for (j = x + 1; j < readlength; j++) {
+        a = q[j];
+        if (a < 4) {
+          or_smem ns = forward_ext(f, smem, a);
+          ns.n = (uint32_t)j;
+          if (ns.s != smem.s) prev[numPrev++] = smem;
+          smem = ns;
+          if (ns.s == 0) break;
+        } else {
+          prev[numPrev++] = smem;
+          break;
+        }
+      }
+      if (smem.s != 0) prev[numPrev++] = smem;
+      for (int p = 0; p < numPrev / 2; p++) {
+        or_smem t = prev[p];
+        prev[p] = prev[numPrev - p - 1];
+        prev[numPrev - p - 1] = t;
+      }
+      int next_x = x - 1, cur_j = readlength;
+      for (j = x - 1; j >= 0; j--) {
+        int numCurr = 0, curr_s = -1;
+        a = q[j];
+        if (a > 3) {
+          next_x = j - 1;
+          break;
+        }
+        for (int p = 0; p < numPrev; p++) {
+          or_smem sm = prev[p];
+          or_smem ns = backward_ext(f, sm, a);
+          ns.m = (uint32_t)j;
+          if (ns.s == 0 && numCurr == 0 && j < cur_j) {
+            cur_j = j;
+            if ((sm.n - sm.m + 1) >= (uint32_t)minSeedLen) matchArray[numTotalSmem[0] + numSmem++] = sm;
+          }
+          if (ns.s != 0 && ns.s != curr_s) {
+            curr_s = (int)ns.s;
+            prev[numCurr++] = ns;
+          }
+        }
+        numPrev = numCurr;
+        if (numCurr == 0) {
+          next_x = j;
+          break;
+        }
+        next_x = j - 1;
+      }
+      if (numPrev != 0) {
+        or_smem sm = prev[0];
+        if ((sm.n - sm.m + 1) >= (uint32_t)minSeedLen) matchArray[numTotalSmem[0] + numSmem++] = sm;
+        numPrev = 0;
+      }
+      x = next_x;
+    }
+    numTotalSmem[0] += numSmem;
+  }
+  free(prev);
+}
+
 /* ctypes-friendly handle API */
 or_fmi *fmi_oracle_new(void) { return (or_fmi *)calloc(1, sizeof(or_fmi)); }
 void fmi_oracle_delete(or_fmi *f) {

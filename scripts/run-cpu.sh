@@ -7,6 +7,8 @@
 # With no benchmark list all four run (phmm, commented out in the reference, is included). dbg, poa,
 # kmer-cnt, pileup and grm are not part of this framework and are reported as
 # skipped. scripts/make-inputs.py writes a synthetic <INPUTS_DIR> in this layout.
+# Optional outputs (unset: the reference's command lines exactly): GB_BSW_OUT=<file> writes bsw's
+# per-pair score/qle/tle/gtle/gscore/max_off lines; GB_PHMM_PRINT=1 prints every phmm result ("%lf").
 set -e
 
 usage() {
@@ -51,11 +53,11 @@ for b in $BENCHES; do
 		;;
 	bsw)
 		echo "Running bsw"
-		"$BIN/bsw" -pairs "$BSW_PAIRS" -t 1 -b 512
+		"$BIN/bsw" -pairs "$BSW_PAIRS" -t 1 -b 512 ${GB_BSW_OUT:+-o "$GB_BSW_OUT"}
 		;;
 	phmm)
 		echo "Running phmm"
-		"$BIN/phmm" -f "$PHMM_IN" -t 1
+		"$BIN/phmm" -f "$PHMM_IN" -t 1 ${GB_PHMM_PRINT:+-p}
 		;;
 	chain)
 		echo "Running chain"

@@ -36,6 +36,9 @@ def _decl(lib):
     lib.fmi_oracle_sa_entries.restype = i64
     lib.fmi_oracle_lf_steps.argtypes = [vp]
     lib.fmi_oracle_lf_steps.restype = i64
+    i32 = ctypes.c_int32
+    lib.fmi_oracle_get_smems.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp]
+    lib.fmi_oracle_get_smems.restype = None
 
 
 class OracleIndex:
@@ -140,6 +143,16 @@ class OracleIndex:
                                              coords.ctypes.data, counts.ctypes.data)
         assert tot == cap
         return coords[:tot], counts[:len(smems)]
+
+    def get_smems(self, codes, num_reads, min_seed_len=19, nthreads=1):
+        """FMI_search::getSMEMs restated (fixed-stride reads of codes.shape[1] bases) -> SMEM array."""
+        codes = np.ascontiguousarray(codes, np.uint8)
+        rl = codes.shape[1]
+        out = np.zeros(max(1, num_reads * (rl + 2) * 2), SMEM_DTYPE)
+        tot = np.zeros(max(1, nthreads), np.int64)
+        self.lib.fmi_oracle_get_smems(self.h, codes.ctypes.data, num_reads, rl, min_seed_len, nthreads,
+                                      out.ctypes.data, tot.ctypes.data)
+        return out[:tot[0]]
 
     def lf_steps(self):
         return self.lib.fmi_oracle_lf_steps(self.h)

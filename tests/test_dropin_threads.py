@@ -15,7 +15,7 @@ from conftest import bits
 from genomicsbench_palisade_amd import gen
 from genomicsbench_palisade_amd._tc import TestcaseArray
 
-MAX_HAPLEN = 9400  # csrc/phmm.hip kMaxHaplen
+MAX_HAPLEN = 65535  # csrc/phmm.hip kMaxHaplen (longer than kLdsHaplen = 9400: records in global scratch)
 
 
 def _phmm_oracle(ta):
@@ -99,7 +99,7 @@ def test_phmm_long_haplotypes_up_to_the_cap():
     phmm.init_pairhmm()
     rng = np.random.default_rng(5)
     pairs = []
-    for hl in (4097, 6000, MAX_HAPLEN):
+    for hl in (4097, 9400, 9401, 20000):
         for rl in (1, 64, 65, 130):
             hap = rng.choice(np.frombuffer(b"ACGT", np.uint8), hl)
             st = int(rng.integers(0, hl - rl + 1))

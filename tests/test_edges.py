@@ -93,22 +93,31 @@ def test_phmm_gpu_edges_bit_exact():
 
 @pytest.mark.gpu
 def test_phmm_gpu_longest_haplotype():
-    """Haplotypes up to kMaxHaplen = 9400 columns (the f64 pass's LDS: 17 bytes per column) are
-    bit-exact; one column more is refused with GB_ERR_ARG (the GKL drop-in then aborts, as documented
-    in include/gb_phmm.h)."""
+    """Haplotypes up to 9400 columns keep their stack's boundary records in LDS (the f64 pass: 17 bytes
+    per column); longer ones -- 9401, 20000 and the 65535 maximum of the 16-bit descriptor field --
+    run on the kLong kernels (records in global scratch), bit-exact against the oracle in both
+    passes, in one batch beside ordinary stacks; 65536 is refused with GB_ERR_ARG (the GKL drop-in
+    then aborts, as documented in include/gb_phmm.h)."""
     from genomicsbench_palisade_amd import GbError, phmm, set_device
     set_device(0)
     phmm.init_pairhmm()
     rng = np.random.default_rng(11)
-    src = rng.choice(ALPHABET[:4], size=9401)
+    src = rng.choice(ALPHABET[:4], size=65536)
     qs = tuple(bytes(v) for v in ([30] * 12, [45] * 12, [45] * 12, [10] * 12))
-    ok = TestcaseArray.from_pairs([((src[500:512].tobytes(),) + qs, src[:9400].tobytes()),
-                                   ((src[9000:9012].tobytes(),) + qs, src[:9400].tobytes())])
+    q40 = tuple(bytes(v) for v in ([40] * 150, [45] * 150, [45] * 150, [10] * 150))
+    pairs = []
+    for hl in (300, 9400, 9401, 20000, 65535):
+        for st in (hl // 3, hl - 12):
+            pairs.append(((src[st:st + 12].tobytes(),) + qs, src[:hl].tobytes()))
+            # a random 150-base read at Q40: far below 1e-28 in f32, so the f64 pass runs it
+            pairs.append(((rng.choice(ALPHABET[:4], size=150).tobytes(),) + q40, src[:hl].tobytes()))
+    ok = TestcaseArray.from_pairs(pairs)
     got = phmm.compute_likelihoods_both(ok)
     exp = phmm_oracle(ok)
+    assert (exp[1] < 1e-28).any() and (exp[1] >= 1e-28).any()  # both passes exercised
     for k in range(3):
-        assert (bits(got[k]) == bits(exp[k])).all()
-    too_long = TestcaseArray.from_pairs([((src[:12].tobytes(),) + qs, src[:9401].tobytes())])
+        assert (bits(got[k]) == bits(exp[k])).all(), k
+    too_long = TestcaseArray.from_pairs([((src[:12].tobytes(),) + qs, (src.tobytes() * 2)[:65536])])
     with pytest.raises(GbError):
         phmm.compute_likelihoods_both(too_long)
 

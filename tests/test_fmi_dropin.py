@@ -32,6 +32,7 @@ MANGLED = [
     "_ZN10FMI_search14get_sa_entriesEP11smem_structPlPijii",
     "_ZN10FMI_search23get_sa_entry_compressedEli", "_ZN10FMI_search13call_one_stepElRlS0_",
     "_ZN10FMI_search23get_sa_entries_prefetchEP11smem_structPlS2_liiRl",
+    "_ZN10FMI_search8getSMEMsEPhiiiiiP11smem_structPl",
 ]
 
 

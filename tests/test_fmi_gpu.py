@@ -157,6 +157,29 @@ def test_heavy_read_pass_exact(fmi, monkeypatch, budget, min_seed, rep):
         assert ctl[4] > 0
 
 
+@pytest.mark.parametrize("nthreads,min_seed,rl", [(1, 19, 151), (3, 19, 151), (1, 8, 70), (7, 12, 101)])
+def test_get_smems_vs_oracle(fmi, nthreads, min_seed, rl):
+    """FMI_search::getSMEMs (FMI_search.cpp:1328-1497, no benchmark caller): the right-to-left search
+    over fixed-stride reads with N's (double push at an N, in-place prev/curr) and the reference's
+    single-thread quota (only the first ceil(numReads / nthreads) reads), bit-exact against the C
+    restatement, SMEMs in the reference's emission order, equal backwardExt counts."""
+    ref = gen.fmi_reference(300_000, seed=61, repeat_frac=0.2)
+    codes, lens = gen.fmi_reads(ref, 700, read_len=rl, seed=62, sub_rate=0.03, n_rate=0.01)
+    codes = np.ascontiguousarray(codes[:, :rl])
+    oi = fmi_util.OracleIndex(ref)
+    c0 = oi.bwt_calls()
+    exp = oi.get_smems(codes, len(codes), min_seed, nthreads)
+    ecalls = oi.bwt_calls() - c0
+    idx = fmi.Index.build(ref)
+    got, calls = idx.get_smems(codes, len(codes), min_seed, nthreads)
+    assert len(exp) > 0
+    assert len(got) == len(exp)
+    assert (smem_tuple_array(got) == smem_tuple_array(exp)).all()
+    assert calls == ecalls
+    assert got["rid"].max() < (len(codes) + nthreads - 1) // nthreads
+    idx.close()
+
+
 def test_cli_dropin(fmi, golden, tmp_path):
     """bin/fmi (CLI of benchmarks/fmi/fmi.cpp: index prefix, FASTQ, batch size, minSeedLen, threads)
     with GB_FMI_PRINT_OUTPUT=1 prints the same SMEMs and per-batch totals as bwa on the golden set."""
