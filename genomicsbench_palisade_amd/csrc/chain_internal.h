@@ -80,13 +80,14 @@ struct gb_chain_batch {
   int32_t *d_sscore = nullptr, *d_sparent = nullptr;  // segment scratch
   int32_t *d_smark = nullptr;     // segment scratch: targets marks of chain_rows' speculative blocks
   uint64_t *d_need = nullptr;     // per chunk: anchors verify_lanes leaves to verify_kernel
+  int32_t *d_slow = nullptr;      // [0]: chunks with such anchors, then their indices (verify_kernel's work list)
   int32_t *d_front = nullptr;     // per split call: first anchor not known to be final
   int32_t *d_fail = nullptr;      // per split call: first anchor whose guess failed verification
   int32_t *d_link[2] = {nullptr, nullptr};  // pointer jumping (chunk-space index or -1)
   int32_t *d_val[2] = {nullptr, nullptr};
   int32_t *d_t2 = nullptr;                 // split anchors' targets marks, merged at the end
   unsigned long long *d_viscall = nullptr; // visited pairs per split call
-  int64_t cap_split = 0, cap_segs = 0, cap_chunks = 0, cap_st = 0, cap_sscore = 0, cap_sparent = 0, cap_smark = 0, cap_need = 0, cap_front = 0,
+  int64_t cap_split = 0, cap_segs = 0, cap_chunks = 0, cap_st = 0, cap_sscore = 0, cap_sparent = 0, cap_smark = 0, cap_need = 0, cap_slow = 0, cap_front = 0,
           cap_jump = 0, cap_t2 = 0, cap_viscall = 0;
   int64_t spec_rounds = 0, fixups = 0;  // statistics of the last run
 };

@@ -20,7 +20,7 @@
 // window iff !(x_i > x_j + max_dist_x) && j >= i - max_iter -- a per-lane predicate on data the lane
 // loads anyway. Other blocks (unsorted calls, fix-ups) stay on chain_kernel.
 //
-// LDS per half: a 128-entry ring of anchors {x, y, score, parent, peak, stamp}. x and y of anchors
+// LDS per half: a 128-entry ring of anchors {x, y, score, parent, peak, stamp} (as five arrays). x and y of anchors
 // [i, i+32) are staged from HBM one 32-anchor block ahead; score/parent/peak enter when an anchor
 // is resolved and leave for HBM 32 anchors at a time; "targets[j] == i" marks of the current anchor are i+1 stamps at the parents' entries
 // (positions >= i-64, the two ring steps). Candidates older than 64 anchors (rare: no break within
@@ -59,8 +59,12 @@ struct RowArgs {
 };
 
 constexpr int kRowRing = 128;           // ring entries per half (anchors [i-64, i+64) are live)
-constexpr int kEnt = 8;                 // words per entry: xlo xhi ylo yhi score parent peak stamp
-constexpr int kHalfWords = kRowRing * kEnt;
+// Per half the ring is five arrays (structure of arrays, word offsets): x and y (2 words per entry),
+// {score, parent}, peak, stamp. Lanes read consecutive entries, so every array is read at its own
+// stride and conflict-free; an interleaved 8-word entry put a step's 32 stamp reads in 4 banks and
+// made 61 % of the kernel's LDS cycles bank conflicts (SQ_LDS_BANK_CONFLICT, profiles/r04b_lds.json).
+constexpr int kXW = 0, kYW = 2 * kRowRing, kSW = 4 * kRowRing, kPW = 6 * kRowRing, kTW = 7 * kRowRing;
+constexpr int kHalfWords = 8 * kRowRing;
 
 // inclusive scans over each 32-lane half: row_shr 1/2/4/8 inside the 16-lane rows, then the even
 // row's lane 15 into the odd row (row_bcast:15 with row_mask 0b1010)
@@ -123,6 +127,7 @@ __device__ __forceinline__ bool geometry32(uint32_t xi_lo, uint32_t yi_lo, uint3
 }
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 typedef int32_t v2i __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
@@ -167,20 +172,38 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
   uint32_t *ring = L + (hi ? kHalfWords : 0);
   uint32_t *dummy = L + 2 * kHalfWords + lane;
 
-  // staged anchors [i, i+32) (lane hl: anchor i + hl), loaded one block ahead
+  // staged anchors: block [b, b+32) (lane hl: anchor b + hl) enters the ring at step b - 1 (block 0
+  // before the loop) from registers loaded one block ahead, so step i can already read anchor i + 1
   uint64_t gx = 0, gy = 0;
   if (hl < n) {
     gx = X[hl];
     gy = Y[hl];
   }
+  auto stage = [&](int32_t b) {
+    const int e = (b + hl) & (kRowRing - 1);
+    v2u ex, ey;
+    ex.x = (uint32_t)gx;
+    ex.y = (uint32_t)(gx >> 32);
+    ey.x = (uint32_t)gy;
+    ey.y = (uint32_t)(gy >> 32);
+    *(v2u *)(ring + kXW + 2 * e) = ex;
+    *(v2u *)(ring + kYW + 2 * e) = ey;
+    const int32_t a = b + 32 + hl;
+    if (a < n) {
+      gx = X[a];
+      gy = Y[a];
+    }
+  };
+  stage(0);
   // anchors [a0, a0+32) of this half (lane hl: a0 + hl) from the ring to the block's outputs
   auto flush = [&](int32_t a0) {
     const int32_t a = a0 + hl;
     if (a < n) {
-      const v4u o = *(const v4u *)(ring + (a & (kRowRing - 1)) * kEnt + 4);
+      const int e = a & (kRowRing - 1);
+      const v2u o = *(const v2u *)(ring + kSW + 2 * e);
       score[a] = (int32_t)o.x;
       parent[a] = (int32_t)o.y;  // row blocks have pbase 0: parents are block-relative in memory too
-      if (fin) peak[a] = (int32_t)o.z;
+      if (fin) peak[a] = (int32_t)ring[kPW + e];
     }
   };
   // targets[p] = i marks: one buffer store per half (the other half's lanes and the lanes with no
@@ -197,30 +220,56 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
     __builtin_amdgcn_raw_buffer_store_b32(i, mr0, (w & !hi) ? off : 0xFFFFFFFFu, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(i, mr1, (w & hi) ? off : 0xFFFFFFFFu, 0, 0);
   };
+  // The score-independent half of a step -- the own anchor, the first 32 candidates' x/y and their
+  // geometry -- is computed one step ahead (it needs no result of the step before), so a step's
+  // dependent chain starts at the candidates' scores: anchor i + 1's geometry is issued before anchor
+  // i's resolution and overlaps its LDS and DPP latencies.
+  auto own = [&](int32_t i) -> v4u {
+    const int e = i & (kRowRing - 1);
+    const v2u mx_ = *(const v2u *)(ring + kXW + 2 * e), my_ = *(const v2u *)(ring + kYW + 2 * e);
+    v4u me;
+    me.x = mx_.x;
+    me.y = mx_.y;
+    me.z = my_.x;
+    me.w = my_.y;
+    return me;
+  };
+  struct Geo {
+    bool valid, ok;
+    int32_t sg;
+  };
+  auto geo_first = [&](int32_t i, const v4u &me) -> Geo {
+    // candidates j = i - 1 - hl (the step's first chunk), as the cs == 0 pass below sees them
+    const bool go = i < (hi ? n1 : n0);
+    const int32_t j = i - 1 - hl;
+    const bool inb = go & (j >= 0) & (j >= i - kMaxIter);
+    const int ej = j & (kRowRing - 1);
+    const v2u gx_ = *(const v2u *)(ring + kXW + 2 * ej), gy_ = *(const v2u *)(ring + kYW + 2 * ej);
+    const uint64_t xi = (uint64_t)me.x | ((uint64_t)me.y << 32);
+    const uint64_t xj = (uint64_t)gx_.x | ((uint64_t)gx_.y << 32);
+    Geo G;
+    G.valid = inb & !(xi > xj + mdx);
+    G.ok = geometry32(me.x, me.z, me.w, gx_.x, gy_.x, gy_.y, G.valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan,
+                      G.sg);
+    return G;
+  };
+  v4u me_n = own(0);
+  Geo geo_n = geo_first(0, me_n);
   // per-half scalars (SGPR pairs): max_f, max_j, visited count
   uint32_t vis0 = 0, vis1 = 0;
   for (int32_t iv = 0; iv < nmax; iv++) {
     const int32_t i = __builtin_amdgcn_readfirstlane(iv);
-    if ((i & 31) == 0) {
-      // results of anchors [i-32, i) from the ring to HBM, 32 per store (the only vmcnt wait of the
-      // common path is the one for the staged anchors below, once per 32 anchors)
-      v4u e;
-      e.x = (uint32_t)gx;
-      e.y = (uint32_t)(gx >> 32);
-      e.z = (uint32_t)gy;
-      e.w = (uint32_t)(gy >> 32);
-      *(v4u *)(ring + ((i + hl) & (kRowRing - 1)) * kEnt) = e;
-      if (i > 0) flush(i - 32);
-      const int32_t a = i + 32 + hl;
-      if (a < n) {
-        gx = X[a];
-        gy = Y[a];
-      }
-    }
+    // results of anchors [i-32, i) from the ring to HBM, 32 per store (the only vmcnt wait of the
+    // common path is the one for the staged anchors, once per 32 anchors)
+    if ((i & 31) == 0 && i > 0) flush(i - 32);
+    if (((i + 1) & 31) == 0) stage(i + 1);
     const bool act0 = i < n0, act1 = i < n1;
     const bool act = hi ? act1 : act0;
-    // own anchor (a broadcast read inside the half)
-    const v4u me = *(const v4u *)(ring + (i & (kRowRing - 1)) * kEnt);
+    // own anchor (a broadcast read inside the half) and its first chunk's geometry, from the step before
+    const v4u me = me_n;
+    const Geo geo = geo_n;
+    me_n = own(i + 1);
+    geo_n = geo_first(i + 1, me_n);
     const uint64_t xi = (uint64_t)me.x | ((uint64_t)me.y << 32);
     const int32_t q_span = (int32_t)(me.w & 0xff);
     int32_t M0 = __builtin_amdgcn_readlane(q_span, 0), M1 = __builtin_amdgcn_readlane(q_span, 32);
@@ -239,21 +288,33 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
       int32_t sg;
       if (cs < 2) {
         // candidates in the ring
-        const uint32_t *ej = ring + (j & (kRowRing - 1)) * kEnt;
-        const v4u g = *(const v4u *)ej;
-        const v2i r = *(const v2i *)(ej + 4);
+        const int ej = j & (kRowRing - 1);
+        const v2u gx_ = *(const v2u *)(ring + kXW + 2 * ej), gy_ = *(const v2u *)(ring + kYW + 2 * ej);
+        v4u g;
+        g.x = gx_.x;
+        g.y = gx_.y;
+        g.z = gy_.x;
+        g.w = gy_.y;
+        const v2i r = *(const v2i *)(ring + kSW + 2 * ej);
         xj = (uint64_t)g.x | ((uint64_t)g.y << 32);
         yj = (uint64_t)g.z | ((uint64_t)g.w << 32);
         fj = r.x;
         pj = r.y;
-        const bool valid = inb & !(xi > xj + mdx);
-        ok = geometry32(me.x, me.z, me.w, g.x, g.z, g.w, valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+        bool valid;
+        if (cs == 0) {  // computed during the step before
+          valid = geo.valid;
+          ok = geo.ok;
+          sg = geo.sg;
+        } else {
+          valid = inb & !(xi > xj + mdx);
+          ok = geometry32(me.x, me.z, me.w, g.x, g.z, g.w, valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
+        }
         // "targets[j] == i": stamps at the parents of this anchor's visited candidates; lanes past
         // the break also stamp, but only positions after the break, which are never read
         const bool writer = ok & (pj >= i - 64) & (pj >= 0);
-        uint32_t *sp = writer ? ring + (pj & (kRowRing - 1)) * kEnt + 7 : dummy;
+        uint32_t *sp = writer ? ring + kTW + (pj & (kRowRing - 1)) : dummy;
         *sp = stamp;
-        tgt = ring[(j & (kRowRing - 1)) * kEnt + 7] == stamp;
+        tgt = ring[kTW + ej] == stamp;
         // (valid is needed below for the visited count)
         const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
         // ---- resolution (shared with the memory path below) ----
@@ -353,7 +414,7 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
     int32_t pkJ = M;
     if (J >= 0) {
       if (J >= i - 64) {
-        pkJ = (int32_t)ring[(J & (kRowRing - 1)) * kEnt + 6];
+        pkJ = (int32_t)ring[kPW + (J & (kRowRing - 1))];
       } else if (hi ? fin1 : fin0) {  // rare: the parent's peak from HBM (final blocks keep peaks)
         __builtin_amdgcn_s_waitcnt(0);
         pkJ = load_l2(peak + J);
@@ -362,12 +423,12 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
     }
     const int32_t pki = (J >= 0 && pkJ > M) ? pkJ : M;
     if (hl == 0 && act) {
-      v4u o;
+      const int e = i & (kRowRing - 1);
+      v2u o;
       o.x = (uint32_t)M;
       o.y = (uint32_t)J;
-      o.z = (uint32_t)pki;
-      o.w = 0u;
-      *(v4u *)(ring + (i & (kRowRing - 1)) * kEnt + 4) = o;
+      *(v2u *)(ring + kSW + 2 * e) = o;
+      ring[kPW + e] = (uint32_t)pki;
     }
   }
   flush((nmax - 1) & ~31);

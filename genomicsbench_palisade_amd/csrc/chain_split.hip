@@ -44,6 +44,15 @@ namespace gbchain {
 
 constexpr int kSegDefault = 4096;   // longest segment
 constexpr int kWarmDefault = 128;   // warm-up anchors before the window of a segment's first anchor
+// A segment's block starts kWarm anchors before the window of its first anchor, but at most kWinCap
+// anchors of that window: the window is every anchor within max_dist_x (up to max_iter = 5000 in
+// dense regions, median ~500 on the bench's sets) while the reference loop stops after ~30
+// candidates (it visits at most 586 on the 'large' set, tests/host walk), so the rest of a wide
+// window only lengthened the block. A loop that does reach past the block start is caught by the
+// verification like any other wrong guess. Measured (tools/chain_knob_probe.py, r04c): cap 512 takes
+// the 1/8 shard from 1.62 to 1.53 ms and 'large' from 5.37 to 5.30 ms with no failed guess; 256 made
+// guesses fail (2 fix-ups on both sets, 3.5 / 7.9 ms).
+constexpr int kWinCapDefault = 512;
 constexpr int kFix = 1024;          // anchors recomputed sequentially after a failed guess
 constexpr int kTagRing = 1024;      // verification stamp ring (tagged, see resolve_tagged)
 
@@ -63,6 +72,8 @@ struct SplitArgs {
   int32_t *t2;                   // the split anchors' targets marks (atomic max), merged at the end
   unsigned long long *viscall;   // visited pairs per split call
   int32_t fault;  // GB_CHAIN_SPLIT_FAULT (tests): guesses of every fault-th anchor are made wrong
+  int32_t *slow;  // [0]: chunks verify_lanes leaves anchors of to verify_kernel, [1..]: the chunks
+  int32_t nch;    // chunks
 };
 
 __device__ __forceinline__ int32_t cidx(const SplitCall &S, int32_t i) { return 64 * S.cbase + (i - S.c1); }
@@ -118,38 +129,52 @@ __global__ __launch_bounds__(256) void jump_round(int64_t n, const int32_t *li, 
   vo[j] = v;
 }
 
-// Links inside one kTile-entry tile of the chunk space first: log2(kTile) doubling rounds in LDS
-// leave every entry with its first link outside its tile (links point to earlier anchors of the same
-// call) and the value folded up to it, so the global rounds that follow count hops between tiles,
-// not anchors: a path of a call of n split anchors crosses at most n / kTile + 2 tiles.
-constexpr int kTile = 1024, kTileLog = 10;
+// Links inside one kTile-entry tile of the chunk space first: doubling rounds in LDS (until no link
+// stays inside the tile, at most log2(kTile)) leave every entry with its first link outside its tile
+// (links point to earlier anchors of the same call) and the value folded up to it, so the global
+// rounds that follow count hops between tiles, not anchors: a path of a call of n split anchors
+// crosses at most n / kTile + 2 tiles. 4096-entry tiles (1024 threads, 4 entries each, 64 KB of
+// LDS): 'large' needs 5 global rounds per direction instead of 8 with 1024-entry tiles.
+constexpr int kTile = 4096, kTileLog = 12, kTileThreads = 1024, kTilePer = kTile / kTileThreads;
 template <int OP>
-__global__ __launch_bounds__(kTile) void jump_local(int64_t nj, int32_t *link, int32_t *val) {
+__global__ __launch_bounds__(kTileThreads) void jump_local(int64_t nj, int32_t *link, int32_t *val) {
   __shared__ int32_t ll[2][kTile], lv[2][kTile];
   const int64_t base = (int64_t)kTile * blockIdx.x;
-  const int32_t t = (int32_t)threadIdx.x;
-  const bool in = base + t < nj;
-  ll[0][t] = in ? link[base + t] : -1;
-  lv[0][t] = in ? val[base + t] : 0;
+#pragma unroll
+  for (int q = 0; q < kTilePer; q++) {
+    const int32_t t = (int32_t)threadIdx.x + q * kTileThreads;
+    const bool in = base + t < nj;
+    ll[0][t] = in ? link[base + t] : -1;
+    lv[0][t] = in ? val[base + t] : 0;
+  }
   __syncthreads();
   int cur = 0;
-#pragma unroll
   for (int r = 0; r < kTileLog; r++) {
-    const int32_t l = ll[cur][t];
-    int32_t v = lv[cur][t], nl = l;
-    if (l >= base && l < base + kTile) {
-      const int32_t w = lv[cur][l - base];
-      v = OP == 0 ? v + w : max(v, w);
-      nl = ll[cur][l - base];
+    int inside = 0;
+#pragma unroll
+    for (int q = 0; q < kTilePer; q++) {
+      const int32_t t = (int32_t)threadIdx.x + q * kTileThreads;
+      const int32_t l = ll[cur][t];
+      int32_t v = lv[cur][t], nl = l;
+      if (l >= base && l < base + kTile) {
+        const int32_t w = lv[cur][l - base];
+        v = OP == 0 ? v + w : max(v, w);
+        nl = ll[cur][l - base];
+        inside |= nl >= base && nl < base + kTile;
+      }
+      ll[cur ^ 1][t] = nl;
+      lv[cur ^ 1][t] = v;
     }
-    ll[cur ^ 1][t] = nl;
-    lv[cur ^ 1][t] = v;
-    __syncthreads();
     cur ^= 1;
+    if (!__syncthreads_or(inside)) break;
   }
-  if (in) {
-    link[base + t] = ll[cur][t];
-    val[base + t] = lv[cur][t];
+#pragma unroll
+  for (int q = 0; q < kTilePer; q++) {
+    const int32_t t = (int32_t)threadIdx.x + q * kTileThreads;
+    if (base + t < nj) {
+      link[base + t] = ll[cur][t];
+      val[base + t] = lv[cur][t];
+    }
   }
 }
 
@@ -240,13 +265,11 @@ __device__ __forceinline__ bool resolve_tagged(int32_t sc, bool ok, int32_t pj, 
 // marks and visited counts are final) uses an 8 K ring, wider than any window (max_iter 5000 + 64
 // lanes), so no mark is ever lost there.
 // need (from verify_lanes): only the anchors whose bit is set (null: all of them).
-template <bool CHECK, int RING = CHECK ? kTagRing : 8192>
-__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const uint64_t *need) {
-  static_assert(CHECK || RING > kMaxIter + 64, "the re-mark ring must hold any window");
-  __shared__ uint32_t S[RING + 64];
-  const uint64_t nd = need ? need[blockIdx.x] : ~0ull;
+template <bool CHECK, int RING>
+__device__ __forceinline__ void verify_chunk(SplitArgs A, const uint64_t *need, int32_t chunk, uint32_t *S) {
+  const uint64_t nd = need ? need[chunk] : ~0ull;
   if (!nd) return;
-  const Chunk ch = A.chunks[blockIdx.x];
+  const Chunk ch = A.chunks[chunk];
   const SplitCall Sc = A.split[ch.sc];
   const int lane = threadIdx.x;
   const int32_t start = ch.start, n = Sc.n;
@@ -273,7 +296,7 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const uint64_t 
   }
   const int32_t ci = min(start + lane, n - 1);
   const uint64_t bx = X[ci], by = Y[ci];
-  const int32_t bf = score[ci], bp = parent[ci], bst = A.st[64 * blockIdx.x + lane];
+  const int32_t bf = score[ci], bp = parent[ci], bst = A.st[64 * chunk + lane];
   const int32_t neg_lane = -lane;
   uint32_t vis = 0;
   int32_t first_bad = INT_MAX;
@@ -319,6 +342,19 @@ __global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const uint64_t 
   }
 }
 
+// With need, the grid walks the work list verify_lanes built (A.slow) instead of one workgroup per
+// chunk (a launch of every chunk's workgroup, nearly all exiting at once, cost 35-45 us a step).
+template <bool CHECK, int RING = CHECK ? kTagRing : 8192>
+__global__ __launch_bounds__(64) void verify_kernel(SplitArgs A, const uint64_t *need) {
+  static_assert(CHECK || RING > kMaxIter + 64, "the re-mark ring must hold any window");
+  __shared__ uint32_t S[RING + 64];
+  const int32_t nwork = need ? A.slow[0] : A.nch;
+  for (int32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const int32_t chunk = need ? A.slow[1 + w] : w;
+    verify_chunk<CHECK, RING>(A, need, chunk, S);
+  }
+}
+
 // 2'. verify, one anchor per lane (the common case, ahead of verify_kernel): lane l re-runs the
 // reference loop of anchor start + l over its first 64 candidates, reading the guessed window from
 // memory (neighbouring lanes read neighbouring anchors), with the "targets[j] == i" marks of its own
@@ -334,6 +370,12 @@ __global__ __launch_bounds__(64) void verify_lanes(SplitArgs A, uint64_t *need) 
   // position instead of one per visited candidate, which made the pass atomic-bound)
   constexpr int kMarkLo = 192, kMarkN = 256;
   __shared__ int32_t lm[kMarkN];
+  // the candidates of the wave's 64 loops (their first 64 each) are anchors [start - 64, start + 63):
+  // staged once into LDS, so each candidate is four LDS reads (consecutive lanes, consecutive
+  // entries: conflict-free) instead of four global loads
+  constexpr int kStage = 128;
+  __shared__ uint64_t cx[kStage], cy[kStage];
+  __shared__ int32_t cf[kStage], cp[kStage];
   const Chunk ch = A.chunks[blockIdx.x];
   const SplitCall Sc = A.split[ch.sc];
   const int lane = threadIdx.x;
@@ -357,6 +399,16 @@ __global__ __launch_bounds__(64) void verify_lanes(SplitArgs A, uint64_t *need) 
   const int32_t fi = score[ii], pi = parent[ii], st = A.st[64 * blockIdx.x + lane];
   const int32_t mbase = start - kMarkLo;
   for (int t = lane; t < kMarkN; t += 64) lm[t] = 0;
+  const int32_t cbase = start - 64;
+  for (int t = lane; t < kStage; t += 64) {
+    const int32_t j = cbase + t;
+    if (j >= 0 && j < n) {
+      cx[t] = X[j];
+      cy[t] = Y[j];
+      cf[t] = score[j];
+      cp[t] = parent[j];
+    }
+  }
   __syncthreads();
   int32_t M = (int32_t)(yi >> 32 & 0xff), J = -1, N = 0;
   uint64_t marks = 0;
@@ -374,10 +426,11 @@ __global__ __launch_bounds__(64) void verify_lanes(SplitArgs A, uint64_t *need) 
       fj[u] = 0;
       pj[u] = -1;
       if (act & (j >= st)) {
-        xj[u] = X[j];
-        yj[u] = Y[j];
-        fj[u] = score[j];
-        pj[u] = parent[j];
+        const int t = j - cbase;  // in [0, 127): j >= i - 64 >= start - 64, j < i <= start + 63
+        xj[u] = cx[t];
+        yj[u] = cy[t];
+        fj[u] = cf[t];
+        pj[u] = cp[t];
       }
     }
 #pragma unroll
@@ -425,25 +478,30 @@ __global__ __launch_bounds__(64) void verify_lanes(SplitArgs A, uint64_t *need) 
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
   if (lane == 0) {
     need[blockIdx.x] = um;
+    if (um) A.slow[1 + atomicAdd(A.slow, 1)] = (int32_t)blockIdx.x;  // verify_kernel's work list
     if (CHECK && bad) atomicMin(A.fail + ch.sc, start + (int32_t)__builtin_ctzll(bad));
     if (v) atomicAdd(A.viscall + ch.sc, (unsigned long long)v);
   }
 }
 
+// peaks of the split anchors, and their targets marks (only split anchors mark them: t2)
 __global__ __launch_bounds__(64) void peak_write(SplitArgs A, const int32_t *pv) {
   const Chunk ch = A.chunks[blockIdx.x];
   const SplitCall S = A.split[ch.sc];
   const int32_t i = ch.start + (int32_t)threadIdx.x;
-  if (i < S.n) A.peak[S.off + i] = pv[64 * blockIdx.x + threadIdx.x];
+  if (i < S.n) {
+    A.peak[S.off + i] = pv[64 * blockIdx.x + threadIdx.x];
+    A.target[S.off + i] = A.t2[S.off + i];
+  }
 }
 
-// targets of a split call: segment 0's own marks (anchors < c1) merged with the split anchors'
-// marks by maximum (the last marker is the largest i); its visited pairs into the total
+// targets of a split call's segment 0 (anchors < c1): its own marks merged with the split anchors'
+// marks by maximum (the last marker is the largest i); the call's visited pairs into the total
 __global__ __launch_bounds__(256) void merge_targets(SplitArgs A) {
   const SplitCall S = A.split[blockIdx.x];
   int32_t *tg = A.target + S.off;
   const int32_t *t2 = A.t2 + S.off;
-  for (int32_t x = threadIdx.x; x < S.n; x += 256) tg[x] = x < S.c1 ? max(tg[x], t2[x]) : t2[x];
+  for (int32_t x = threadIdx.x; x < S.c1; x += 256) tg[x] = max(tg[x], t2[x]);
   if (threadIdx.x == 0) atomicAdd(A.visited, A.viscall[blockIdx.x]);
 }
 
@@ -465,7 +523,7 @@ int grow(T **p, int64_t *cap, int64_t need) {
 // under the batch's throughput time, so small batches get shorter segments; shorter ones cost more
 // verification and warm-up work. GB_CHAIN_SPLIT: "0" runs every call whole; "SEG[,WARM]" sets the segment length and warm-up
 // (tests force tiny segments without warm-up to exercise the fix-up path).
-void split_knobs(int64_t total_anchors, int *seg, int *warm, int *trunc) {
+void split_knobs(int64_t total_anchors, int *seg, int *warm, int *trunc, int *wcap) {
   // the power of two in [512, 4096] nearest below total / 12 000 (measured with chain_rows,
   // tools/chain_rows_probe.py: 'large' 25.4 M anchors 2048 (7.76 ms; 4096 7.87, 1024 10.3), 'small'
   // 2.5 M and the 1/8 shard 3.2 M anchors 512 (2.06 / 2.20 ms; 1024 2.29 / 2.38)
@@ -473,13 +531,15 @@ void split_knobs(int64_t total_anchors, int *seg, int *warm, int *trunc) {
   while (*seg > 512 && (int64_t)*seg * 12000 > total_anchors) *seg /= 2;
   *warm = kWarmDefault;
   *trunc = 0;
+  *wcap = kWinCapDefault;
   const char *e = getenv("GB_CHAIN_SPLIT");
   if (!e || !*e) return;
-  int a = 0, b = -1, t = 0;
-  const int k = sscanf(e, "%d,%d,%d", &a, &b, &t);
-  if (k >= 1) *seg = a;
+  int a = 0, b = -1, t = 0, w = -1;
+  const int k = sscanf(e, "%d,%d,%d,%d", &a, &b, &t, &w);
+  if (k >= 1 && a >= 0) *seg = a;  // -1: the adaptive length
   if (k >= 2 && b >= 0) *warm = b;
   if (k >= 3) *trunc = t;
+  if (k >= 4 && w >= 0) *wcap = w;
 }
 
 SplitArgs split_args(gb_chain_batch *B) {
@@ -506,6 +566,8 @@ SplitArgs split_args(gb_chain_batch *B) {
   A.viscall = B->d_viscall;
   const char *f = getenv("GB_CHAIN_SPLIT_FAULT");
   A.fault = f ? atoi(f) : 0;
+  A.slow = B->d_slow;
+  A.nch = (int32_t)B->chunks.size();
   return A;
 }
 
@@ -522,9 +584,9 @@ int jump(gb_chain_batch *B, int op, int rounds) {
   const unsigned g = (unsigned)((nj + 255) / 256);
   const unsigned nt = (unsigned)((nj + kTile - 1) / kTile);
   if (op == 0)
-    hipLaunchKernelGGL(jump_local<0>, dim3(nt), dim3(kTile), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
+    hipLaunchKernelGGL(jump_local<0>, dim3(nt), dim3(kTileThreads), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
   else
-    hipLaunchKernelGGL(jump_local<1>, dim3(nt), dim3(kTile), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
+    hipLaunchKernelGGL(jump_local<1>, dim3(nt), dim3(kTileThreads), 0, B->stream, nj, B->d_link[0], B->d_val[0]);
   int cur = 0;
   for (int r = 0; r < rounds; r++) {
     if (op == 0)
@@ -541,8 +603,8 @@ int jump(gb_chain_batch *B, int op, int rounds) {
 }  // namespace
 
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4) {
-  int seg, warm, trunc;
-  split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm, &trunc);
+  int seg, warm, trunc, wcap;
+  split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm, &trunc, &wcap);
   const int64_t ncalls = B->ncalls;
   B->vc.clear();
   B->split.clear();
@@ -614,7 +676,8 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
             // trunc: the warm-up starts `warm` anchors before c_s whatever the window (the first
             // anchors' spec loops then miss their oldest candidates, which only matters -- and is
             // then caught by the verification -- for loops that would have reached them)
-            const int32_t a = k == 0 ? 0 : std::max(0, trunc ? cs - warm : K.st[(size_t)cs] - warm);
+            const int32_t a =
+                k == 0 ? 0 : std::max(0, trunc ? cs - warm : std::max(K.st[(size_t)cs], cs - wcap) - warm);
             int32_t w = 0;
             for (int32_t i = a; i < es; i++) w = std::max(w, i - std::max(a, K.st[(size_t)i]));
             K.as[(size_t)k] = a;
@@ -697,6 +760,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   if (!st) st = grow(&B->d_viscall, &B->cap_viscall, ns);
   if (!st) st = grow(&B->d_t2, &B->cap_t2, B->nanchors);
   if (!st) st = grow(&B->d_need, &B->cap_need, nch);
+  if (!st) st = grow(&B->d_slow, &B->cap_slow, nch + 1);
   if (st) return st;
   B->d_fail = B->d_front + ns;
   {
@@ -737,6 +801,8 @@ int split_resolve(gb_chain_batch *B) {
   // GB_CHAIN_VLANES=0: verify_kernel alone (A/B and tests)
   const char *vl = getenv("GB_CHAIN_VLANES");
   const bool lanes = !(vl && vl[0] == '0');
+  // verify_kernel's persistent grid over verify_lanes' work list: 4 waves per SIMD
+  const unsigned slow_grid = std::max(1u, std::min(nch, (unsigned)(16 * dev_limits().cus)));
   std::vector<VCall> fix;
   std::vector<uint8_t> failed((size_t)ns, 0);
   B->spec_rounds = 0;
@@ -748,8 +814,9 @@ int split_resolve(gb_chain_batch *B) {
     hipLaunchKernelGGL(guess_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
     GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
     if (lanes) {
+      GB_HIP(hipMemsetAsync(B->d_slow, 0, sizeof(int32_t), B->stream));
       hipLaunchKernelGGL(verify_lanes<true>, dim3(nch), dim3(64), 0, B->stream, A, B->d_need);
-      hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
+      hipLaunchKernelGGL(verify_kernel<true>, dim3(slow_grid), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
     } else {
       hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)nullptr);
     }
@@ -793,8 +860,9 @@ int split_resolve(gb_chain_batch *B) {
   if (redo) {
     GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
     if (lanes) {
+      GB_HIP(hipMemsetAsync(B->d_slow, 0, sizeof(int32_t), B->stream));
       hipLaunchKernelGGL(verify_lanes<false>, dim3(nch), dim3(64), 0, B->stream, A, B->d_need);
-      hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
+      hipLaunchKernelGGL(verify_kernel<false>, dim3(slow_grid), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
     } else {
       hipLaunchKernelGGL(verify_kernel<false>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)nullptr);
     }
@@ -812,7 +880,7 @@ void split_free(gb_chain_batch *B) {
   for (void *p : {(void *)B->d_vc, (void *)B->d_split, (void *)B->d_segs, (void *)B->d_chunks, (void *)B->d_st,
                   (void *)B->d_sscore, (void *)B->d_sparent, (void *)B->d_front, (void *)B->d_link[0],
                   (void *)B->d_link[1], (void *)B->d_val[0], (void *)B->d_val[1], (void *)B->d_t2,
-                  (void *)B->d_viscall, (void *)B->d_smark, (void *)B->d_need})
+                  (void *)B->d_viscall, (void *)B->d_smark, (void *)B->d_need, (void *)B->d_slow})
     (void)hipFree(p);
   B->d_vc = nullptr;
 }

@@ -163,8 +163,8 @@ __device__ void heap_sort(gb_smem *a, int n) {
 // the read (one pass of dword loads from the nibble-packed copy d_q4), so the base lookups of the
 // state machine are LDS reads instead of dependent global byte loads. Longer reads read d_qdb.
 // 152 bases (the reference's 151-bp reads): 19 words per lane row, odd, so same-word reads are
-// conflict-free, and with the 8 KB `prev` list head (kTop) a wave's LDS is 13 056 B -- 12 waves per
-// CU in 512-B allocation granules (160 bases' 21-word rows made it 13 568 B: 11 waves)
+// conflict-free, and with the 8 KB `prev` list head (kTop) a wave's LDS is 13 056 B, of which 12
+// fit a CU's 160 KB (the grid runs 11 per CU, lanes_for_device)
 constexpr int kQBases = 152;
 constexpr int kQW = kQBases / 8;
 static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
@@ -884,7 +884,8 @@ struct gb_fmi_reads {
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   int32_t nreads = 0, stride = 0;
-  int lanes = 0;
+  int lanes = 0;  // resident lanes of the persistent search grid
+  int cus = 256;
   uint8_t *d_qdb = nullptr;
   uint32_t *d_q4 = nullptr;
   int32_t q4_stride = 0;
@@ -920,16 +921,20 @@ struct gb_fmi_reads {
 
 namespace {
 
-int lanes_for_device() {
+int device_cus() {
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  return cus;
+}
+
+int lanes_for_device(int cus) {
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
-  // 11 resident waves per CU: the most the LDS holds with the staged read codes and the 8-entry
-  // `prev` list head (13 056 B per wave in 2 KB allocation granules). Round 2 chose 12 (3 per SIMD)
-  // over 16 (tools/fmi_small_occ.sh); the read codes from global memory instead (GB_FMI_QLDS=0)
-  // allow 16 but ran slower: 4 M reads 115 ms at 16 waves vs 111 ms staged at 11 (r03m).
+  // 11 workgroups (waves) per CU in the persistent grid: 13 056 B of LDS per wave (the staged read
+  // codes and the 8-entry `prev` list head) would fit 12 in 160 KB; 11 measured best of 8 / 11 in
+  // r03m and 11 vs 12 is within noise (r04, tools/gpu_adhoc runs). The read codes from global memory
+  // instead (GB_FMI_QLDS=0) allow 16 but ran slower: 4 M reads 115 ms at 16 waves vs 111 ms staged.
   const int waves = e ? std::max(1, atoi(e)) : 11;
   return cus * waves * 64;
 }
@@ -1213,7 +1218,8 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   R->idx = idx;
   R->nreads = num_reads;
   R->stride = max_readlength;
-  R->lanes = lanes_for_device();
+  R->cus = device_cus();
+  R->lanes = lanes_for_device(R->cus);
   R->ran = R->scattered = false;
   R->total = 0;
   const size_t nr = (size_t)std::max(num_reads, 1);
@@ -1385,7 +1391,7 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
       H.bwt_calls = A.bwt_calls;
       H.trace = A.trace;
       // the heavy-read count is on the device: a grid of 16 waves per CU strides over the list
-      hipLaunchKernelGGL(gbfmi::smem_heavy, dim3((unsigned)std::max(1, R->lanes / 64 * 16 / 12)), dim3(64), 0,
+      hipLaunchKernelGGL(gbfmi::smem_heavy, dim3((unsigned)std::max(1, R->cus * 16)), dim3(64), 0,
                          R->stream, H);
       GB_HIP(hipGetLastError());
     }

@@ -142,11 +142,13 @@ def split_calls():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("split,fault,rows", [("", 0, "1"), ("0", 0, "1"), ("256,0", 0, "1"), ("64,0", 0, "1"),
-                                              ("128,8", 37, "1"), ("", 997, "1"), ("", 0, "0"), ("128,8", 37, "0")])
+                                              ("128,8", 37, "1"), ("", 997, "1"), ("", 0, "0"), ("128,8", 37, "0"),
+                                              ("256,32,0,16", 0, "1"), ("-1,128,0,5000", 0, "1")])
 def test_gpu_split_exact(split_calls, monkeypatch, split, fault, rows):
     """Long calls as speculative segments (csrc/chain_split.hip) give the sequential loop's results
-    bit for bit: default and tiny segments, no warm-up, and injected wrong guesses that the
-    verification must catch and the sequential fix-up repair."""
+    bit for bit: default and tiny segments, no warm-up, injected wrong guesses that the verification
+    must catch and the sequential fix-up repair, a 16-anchor window cap (blocks start far inside
+    their first anchor's window, so guesses fail for real) and the uncapped window."""
     from genomicsbench_palisade_amd import chain, set_device
     set_device(0)
     calls, exp = split_calls
@@ -163,7 +165,7 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault, rows):
         assert ns == 0
     else:
         # default: the segment length adapts to the batch (512..4096 anchors, chain_split.hip)
-        seg = int(split.split(",")[0]) if split else 512
+        seg = int(split.split(",")[0]) if split and not split.startswith("-") else 512
         long_calls = sum(1 for c in range(calls.ncalls) if calls.offsets[c + 1] - calls.offsets[c] >= 2 * seg)
         assert 0 < ns < long_calls  # the unsorted long call stays whole
     if fault:

@@ -10,6 +10,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import genomicsbench_palisade_amd as g  # noqa: E402
+if os.environ.get("CHAIN_LIB"):  # another build of libgb.so, to time two builds on one box
+    g.LIBGB = os.path.abspath(os.environ["CHAIN_LIB"])
 from genomicsbench_palisade_amd import chain, gen, set_device, shard  # noqa: E402
 
 set_device(0)
@@ -49,5 +52,5 @@ for name, calls in sets:
         if base is None:
             base = r
         same = all(np.array_equal(a, b) for a, b in zip(base[:4], r[:4])) and base[4] == r[4]
-        print(f"{name:9s} [{cfg or 'default':40s}] {t:7.3f} ms ({calls.nanchors / t / 1e3:7.1f} Manchors/s) "
+        print(f"{os.path.basename(g.LIBGB)} {name:9s} [{cfg or 'default':40s}] {t:7.3f} ms ({calls.nanchors / t / 1e3:7.1f} Manchors/s) "
               f"split calls/rounds/fix-ups {st} same={same}", flush=True)
