@@ -172,29 +172,16 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
   uint32_t *ring = L + (hi ? kHalfWords : 0);
   uint32_t *dummy = L + 2 * kHalfWords + lane;
 
-  // staged anchors: block [b, b+32) (lane hl: anchor b + hl) enters the ring at step b - 1 (block 0
-  // before the loop) from registers loaded one block ahead, so step i can already read anchor i + 1
+  // staged anchors [i, i+32) (lane hl: anchor i + hl), loaded one block ahead
   uint64_t gx = 0, gy = 0;
   if (hl < n) {
     gx = X[hl];
     gy = Y[hl];
   }
-  auto stage = [&](int32_t b) {
-    const int e = (b + hl) & (kRowRing - 1);
-    v2u ex, ey;
-    ex.x = (uint32_t)gx;
-    ex.y = (uint32_t)(gx >> 32);
-    ey.x = (uint32_t)gy;
-    ey.y = (uint32_t)(gy >> 32);
-    *(v2u *)(ring + kXW + 2 * e) = ex;
-    *(v2u *)(ring + kYW + 2 * e) = ey;
-    const int32_t a = b + 32 + hl;
-    if (a < n) {
-      gx = X[a];
-      gy = Y[a];
-    }
-  };
-  stage(0);
+  // stamps are i + 1 >= 1: clear the half's stamp array, which holds whatever the CU's previous
+  // workgroup left in this LDS (a stale value equal to i + 1 read as a mark made results depend on
+  // what ran before; seen as a flaky targets / visited mismatch)
+  for (int t = hl; t < kRowRing; t += 32) ring[kTW + t] = 0u;
   // anchors [a0, a0+32) of this half (lane hl: a0 + hl) from the ring to the block's outputs
   auto flush = [&](int32_t a0) {
     const int32_t a = a0 + hl;
@@ -220,56 +207,40 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
     __builtin_amdgcn_raw_buffer_store_b32(i, mr0, (w & !hi) ? off : 0xFFFFFFFFu, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(i, mr1, (w & hi) ? off : 0xFFFFFFFFu, 0, 0);
   };
-  // The score-independent half of a step -- the own anchor, the first 32 candidates' x/y and their
-  // geometry -- is computed one step ahead (it needs no result of the step before), so a step's
-  // dependent chain starts at the candidates' scores: anchor i + 1's geometry is issued before anchor
-  // i's resolution and overlaps its LDS and DPP latencies.
-  auto own = [&](int32_t i) -> v4u {
-    const int e = i & (kRowRing - 1);
-    const v2u mx_ = *(const v2u *)(ring + kXW + 2 * e), my_ = *(const v2u *)(ring + kYW + 2 * e);
-    v4u me;
-    me.x = mx_.x;
-    me.y = mx_.y;
-    me.z = my_.x;
-    me.w = my_.y;
-    return me;
-  };
-  struct Geo {
-    bool valid, ok;
-    int32_t sg;
-  };
-  auto geo_first = [&](int32_t i, const v4u &me) -> Geo {
-    // candidates j = i - 1 - hl (the step's first chunk), as the cs == 0 pass below sees them
-    const bool go = i < (hi ? n1 : n0);
-    const int32_t j = i - 1 - hl;
-    const bool inb = go & (j >= 0) & (j >= i - kMaxIter);
-    const int ej = j & (kRowRing - 1);
-    const v2u gx_ = *(const v2u *)(ring + kXW + 2 * ej), gy_ = *(const v2u *)(ring + kYW + 2 * ej);
-    const uint64_t xi = (uint64_t)me.x | ((uint64_t)me.y << 32);
-    const uint64_t xj = (uint64_t)gx_.x | ((uint64_t)gx_.y << 32);
-    Geo G;
-    G.valid = inb & !(xi > xj + mdx);
-    G.ok = geometry32(me.x, me.z, me.w, gx_.x, gy_.x, gy_.y, G.valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan,
-                      G.sg);
-    return G;
-  };
-  v4u me_n = own(0);
-  Geo geo_n = geo_first(0, me_n);
   // per-half scalars (SGPR pairs): max_f, max_j, visited count
   uint32_t vis0 = 0, vis1 = 0;
   for (int32_t iv = 0; iv < nmax; iv++) {
     const int32_t i = __builtin_amdgcn_readfirstlane(iv);
-    // results of anchors [i-32, i) from the ring to HBM, 32 per store (the only vmcnt wait of the
-    // common path is the one for the staged anchors, once per 32 anchors)
-    if ((i & 31) == 0 && i > 0) flush(i - 32);
-    if (((i + 1) & 31) == 0) stage(i + 1);
+    if ((i & 31) == 0) {
+      // results of anchors [i-32, i) from the ring to HBM, 32 per store (the only vmcnt wait of the
+      // common path is the one for the staged anchors below, once per 32 anchors)
+      const int e = (i + hl) & (kRowRing - 1);
+      v2u ex, ey;
+      ex.x = (uint32_t)gx;
+      ex.y = (uint32_t)(gx >> 32);
+      ey.x = (uint32_t)gy;
+      ey.y = (uint32_t)(gy >> 32);
+      *(v2u *)(ring + kXW + 2 * e) = ex;
+      *(v2u *)(ring + kYW + 2 * e) = ey;
+      if (i > 0) flush(i - 32);
+      const int32_t a = i + 32 + hl;
+      if (a < n) {
+        gx = X[a];
+        gy = Y[a];
+      }
+    }
     const bool act0 = i < n0, act1 = i < n1;
     const bool act = hi ? act1 : act0;
-    // own anchor (a broadcast read inside the half) and its first chunk's geometry, from the step before
-    const v4u me = me_n;
-    const Geo geo = geo_n;
-    me_n = own(i + 1);
-    geo_n = geo_first(i + 1, me_n);
+    // own anchor (a broadcast read inside the half)
+    v4u me;
+    {
+      const int e = i & (kRowRing - 1);
+      const v2u mx_ = *(const v2u *)(ring + kXW + 2 * e), my_ = *(const v2u *)(ring + kYW + 2 * e);
+      me.x = mx_.x;
+      me.y = mx_.y;
+      me.z = my_.x;
+      me.w = my_.y;
+    }
     const uint64_t xi = (uint64_t)me.x | ((uint64_t)me.y << 32);
     const int32_t q_span = (int32_t)(me.w & 0xff);
     int32_t M0 = __builtin_amdgcn_readlane(q_span, 0), M1 = __builtin_amdgcn_readlane(q_span, 32);
@@ -300,15 +271,8 @@ __global__ __launch_bounds__(64) void chain_rows(RowArgs A) {
         yj = (uint64_t)g.z | ((uint64_t)g.w << 32);
         fj = r.x;
         pj = r.y;
-        bool valid;
-        if (cs == 0) {  // computed during the step before
-          valid = geo.valid;
-          ok = geo.ok;
-          sg = geo.sg;
-        } else {
-          valid = inb & !(xi > xj + mdx);
-          ok = geometry32(me.x, me.z, me.w, g.x, g.z, g.w, valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
-        }
+        const bool valid = inb & !(xi > xj + mdx);
+        ok = geometry32(me.x, me.z, me.w, g.x, g.z, g.w, valid, max_dist_x, max_dist_y, bw, n_segs, avg_qspan, sg);
         // "targets[j] == i": stamps at the parents of this anchor's visited candidates; lanes past
         // the break also stamp, but only positions after the break, which are never read
         const bool writer = ok & (pj >= i - 64) & (pj >= 0);

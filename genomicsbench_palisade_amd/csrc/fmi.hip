@@ -929,13 +929,20 @@ int device_cus() {
   return cus;
 }
 
+// `prev` list head entries kept in LDS (GB_FMI_TOP: 8, 4 or 0)
+int top_entries() {
+  const char *te = getenv("GB_FMI_TOP");
+  return te ? atoi(te) : 4;
+}
+
 int lanes_for_device(int cus) {
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
-  // 11 workgroups (waves) per CU in the persistent grid: 13 056 B of LDS per wave (the staged read
-  // codes and the 8-entry `prev` list head) would fit 12 in 160 KB; 11 measured best of 8 / 11 in
-  // r03m and 11 vs 12 is within noise (r04, tools/gpu_adhoc runs). The read codes from global memory
-  // instead (GB_FMI_QLDS=0) allow 16 but ran slower: 4 M reads 115 ms at 16 waves vs 111 ms staged.
-  const int waves = e ? std::max(1, atoi(e)) : 11;
+  // Waves (workgroups) per CU of the persistent grid. LDS per wave is the staged read codes (4.9 KB)
+  // plus the `prev` list head (2 KB per entry kept); 116 VGPRs allow 4 waves per SIMD. With an
+  // 8-entry head (13 KB) 12 fit and 11 / 12 run alike; a 4-entry head (8.9 KB) lets the VGPR limit,
+  // 16, bind, which hides more gather latency than the 4 extra LDS entries save: 10 M reads 248 vs
+  // 260 ms, the 1/8 shard 35.8 vs 36.7 ms (tools/fmi_knob_probe.py, profiles/r04e_fmi_knobs.log).
+  const int waves = e ? std::max(1, atoi(e)) : (top_entries() >= 8 ? 11 : 16);
   return cus * waves * 64;
 }
 
@@ -1350,9 +1357,8 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     A.list = nullptr;
     A.list_n = nullptr;
     const int blocks = std::max(1, std::min(R->lanes / 64, (R->nreads + 63) / 64));
-    // GB_FMI_TOP: entries of the `prev` list head kept in LDS, 8 (default), 4 or 0
-    const char *te = getenv("GB_FMI_TOP");
-    const int top = te ? atoi(te) : 8;
+    // entries of the `prev` list head kept in LDS, 4 (default), 8 or 0
+    const int top = top_entries();
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, R->stream, A); };
     const char *qe = getenv("GB_FMI_QLDS");  // 0: read codes from global memory, not staged in LDS
     if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0')) {
