@@ -53,6 +53,23 @@ BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar in
 PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
+def source_digest() -> str:
+    """sha256 (16 hex) of the kernel sources (csrc/ and include/): tools/pmc_summary.py stamps it into
+    each profiles/*_pmc.json, and a bench line's traffic_detail says whether its counters were taken
+    on the code being measured ("stale": false) or on other code (true; null for a file without it)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "genomicsbench_palisade_amd", "csrc", "*"))
+                   + glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*", "*.h")))
+    for f in files:
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(os.path.relpath(f, ROOT).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic_detail(kernel: str, leg: str = ""):
     """Per-launch HBM bytes of `kernel` from the newest committed profiles/*_pmc.json (rocprofv3
     FETCH_SIZE and WRITE_SIZE passes of this same bench configuration, tools/gpu_prof.sh +
@@ -80,7 +97,8 @@ def pmc_traffic_detail(kernel: str, leg: str = ""):
             return {"bytes": k["fetch_bytes"] + k["write_bytes"], "fetch_bytes": k["fetch_bytes"],
                     "fetch_bytes_raw": k["fetch_bytes_raw"], "fetch_factor": k["fetch_factor"],
                     "fetch_class": k["fetch_class"], "write_bytes": k["write_bytes"],
-                    "source": os.path.relpath(f, ROOT)}
+                    "source": os.path.relpath(f, ROOT),
+                    "stale": (d["_code"] != source_digest()) if "_code" in d else None}
     return None
 
 
@@ -361,6 +379,10 @@ def _roof_short(r):
     out = _pick(r, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic"))
     if out and isinstance(out.get("kernel"), str):
         out["kernel"] = out["kernel"].split(" ")[0]
+    td = r.get("traffic_detail") if isinstance(r, dict) else None
+    if out and out.get("traffic") is not None and isinstance(td, dict):
+        # counters taken on other kernel code than the one measured: say so beside the number
+        out["traffic_stale"] = td.get("stale")
     return out
 
 

@@ -55,3 +55,29 @@ def test_headline_partial_legs():
     h = bench.headline(d)
     assert h["fmi"] is None and h["roofline"]["frac"] > 0
     json.dumps(h)
+
+
+def test_pmc_traffic_marks_other_code_stale(tmp_path, monkeypatch):
+    # counters stamped with the current sources' digest are current; any other stamp is stale, and a
+    # file without one is "unknown" (None); the headline carries the mark beside the number
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"fetch_bytes": 2.0, "fetch_bytes_raw": 1.0, "fetch_factor": 2.0, "fetch_class": "stream",
+             "write_bytes": 1.0}
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "source_digest", lambda: "abc")
+    (prof / "r09a_pmc.json").write_text(json.dumps({"k": entry}))
+    assert bench.pmc_traffic_detail("k")["stale"] is None
+    (prof / "r09b_pmc.json").write_text(json.dumps({"k": entry, "_code": "old"}))
+    assert bench.pmc_traffic_detail("k")["stale"] is True
+    (prof / "r09c_pmc.json").write_text(json.dumps({"k": entry, "_code": "abc"}))
+    td = bench.pmc_traffic_detail("k")
+    assert td["stale"] is False and td["bytes"] == 3.0 and td["source"] == os.path.join("profiles", "r09c_pmc.json")
+    r = bench._roof_short({"bound": "hbm", "achieved": 1.0, "peak": 2.0, "unit": "GB/s", "frac": 0.5,
+                           "traffic": 3.0, "traffic_detail": td})
+    assert r["traffic_stale"] is False
+
+
+def test_source_digest_is_stable():
+    assert bench.source_digest() == bench.source_digest()
+    assert len(bench.source_digest()) == 16

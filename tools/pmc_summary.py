@@ -87,6 +87,9 @@ def main():
         res[k] = {"launches": len(fb), "fetch_bytes": raw * FETCH_FACTOR[cls], "fetch_bytes_raw": raw,
                   "fetch_class": cls, "fetch_factor": FETCH_FACTOR[cls],
                   "write_bytes": sum(wb) / max(len(wb), 1), "mean_ms_under_pmc": sum(ms) / max(len(ms), 1)}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import source_digest
+    res["_code"] = source_digest()  # bench.py marks traffic from other code "stale"
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch; fetch "
                     "scaled by the calibrated factor of the kernel's read class (tools/probes/pmc_calib.hip, "
                     "profiles/r01g_pmc_calib.txt), write exact")
