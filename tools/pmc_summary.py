@@ -18,7 +18,7 @@ import sys
 
 HOT = {"phmm_forward<float": "phmm_forward<float>", "phmm_forward<double": "phmm_forward<double>",
        "smem_search": "smem_search", "chain_kernel": "chain_kernel", "chain_rows": "chain_rows", "verify_lanes": "verify_lanes", "bsw_extend_kernel": "bsw_extend_kernel",
-       "bsw_lane_kernel": "bsw_lane_kernel", "sa_walk": "sa_walk"}
+       "bsw_lane_kernel": "bsw_lane_kernel", "sa_walk": "sa_walk", "smem_heavy": "smem_heavy"}
 
 FETCH_FACTOR = {"gather": 1.0, "stream": 2.0}
 # dominant read class per kernel: scattered per-lane line requests ("gather") or coalesced

@@ -59,6 +59,9 @@ constexpr int kIters = 4096;
 #define OP_MULF_ROR(r) asm volatile("v_mul_f32_dpp %0, %0, %1 wave_ror:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define OP_ADDF_DPP(r) asm volatile("v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define OP_ADDF64(r) asm volatile("v_add_f64 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
+#define OP_MULF64(r) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
+#define OP_PKADDF(r) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
+#define OP_PKFMAF(r) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
 
 KERNEL(k_addf, OP_ADDF, 0x3f800000u)
 KERNEL(k_mulf, OP_MULF, 0x3f800000u)
@@ -93,6 +96,31 @@ KERNEL(k_mulf_dpp, OP_MULF_DPP, 0x3f800000u)
 KERNEL(k_mulf_ror, OP_MULF_ROR, 0x3f800000u)
 KERNEL(k_addf_dpp, OP_ADDF_DPP, 0x3f800000u)
 
+#define KERNEL64(NAME, OP)                                                                          \
+  __global__ __launch_bounds__(256) void NAME(uint32_t *out, unsigned long long *clk, uint32_t s) {  \
+    double a0 = threadIdx.x + s, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 + 9, a5 = a0 + 11,     \
+           a6 = a0 + 13, a7 = a0 + 17;                                                              \
+    double kd = 1.0;                                                                                \
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();                                    \
+    for (int i = 0; i < kIters; i++) { BODY8(OP) }                                                 \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();                                    \
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7);        \
+    if (threadIdx.x == 0) atomicMax(clk, t1 - t0);                                                 \
+  }
+#define OP64(INS) asm volatile(INS " %0, %0, %1" : "+v"(r) : "v"(kd));
+#define OP_D_ADDF64(r) asm volatile("v_add_f64 %0, %0, %1" : "+v"(r) : "v"(kd));
+#define OP_D_MULF64(r) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(r) : "v"(kd));
+#define OP_D_FMAF64(r) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(r) : "v"(kd));
+#define OP_D_PKMULF(r) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(r) : "v"(kd));
+#define OP_D_PKADDF(r) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(r) : "v"(kd));
+#define OP_D_PKFMAF(r) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(r) : "v"(kd));
+KERNEL64(k_addf64, OP_D_ADDF64)
+KERNEL64(k_mulf64, OP_D_MULF64)
+KERNEL64(k_fmaf64, OP_D_FMAF64)
+KERNEL64(k_pkmulf, OP_D_PKMULF)
+KERNEL64(k_pkaddf, OP_D_PKADDF)
+KERNEL64(k_pkfmaf, OP_D_PKFMAF)
+
 typedef void (*KFN)(uint32_t *, unsigned long long *, uint32_t);
 
 int main() {
@@ -109,7 +137,9 @@ int main() {
       {"v_bfe_i32", k_bfe}, {"v_mov_b32", k_mov}, {"v_sub_f32", k_subf}, {"v_fmac_f32", k_fmac},
       {"v_max_f32", k_maxf}, {"v_add_u16", k_addi16}, {"v_lshl_or_b32", k_lshlor},
       {"cmp+cndmask(vcc)x2", k_cmpcnd}, {"cndmask(sgpr)", k_cnds}, {"v_cmp(vcc)", k_cmp},
-      {"v_mul_f32_dpp row_shr", k_mulf_dpp}, {"v_mul_f32_dpp wave_ror", k_mulf_ror}, {"v_add_f32_dpp row_shr", k_addf_dpp}};
+      {"v_mul_f32_dpp row_shr", k_mulf_dpp}, {"v_mul_f32_dpp wave_ror", k_mulf_ror}, {"v_add_f32_dpp row_shr", k_addf_dpp},
+      {"v_add_f64", k_addf64}, {"v_mul_f64", k_mulf64}, {"v_fma_f64", k_fmaf64}, {"v_pk_mul_f32", k_pkmulf},
+      {"v_pk_add_f32", k_pkaddf}, {"v_pk_fma_f32", k_pkfmaf}};
   for (auto &k : ks) {
     for (int rep = 0; rep < 2; rep++) {
       CK(hipMemset(clk, 0, 8));
