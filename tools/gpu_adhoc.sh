@@ -4,10 +4,6 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=r04k
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_chain.py -m gpu > gpurun_out/chain_tests_$T.log 2>&1 || { tail -30 gpurun_out/chain_tests_$T.log; exit 1; }
-tail -2 gpurun_out/chain_tests_$T.log
-for rep in 1 2; do
-  CHAIN_LIB=genomicsbench_palisade_amd/lib/ab/libgb_old.so timeout -k 10 200 python3 tools/chain_knob_probe.py 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/chain_ab_$T.log || exit 1
-  timeout -k 10 200 python3 tools/chain_knob_probe.py 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/chain_ab_$T.log || exit 1
-done
+T=r04l
+PROBE_VARIANTS="base:;wg12:GB_PHMM_F64_WG=12;wg17:GB_PHMM_F64_WG=17;wg20:GB_PHMM_F64_WG=20;wg24:GB_PHMM_F64_WG=24;wg32:GB_PHMM_F64_WG=32" \
+  timeout -k 10 300 python3 tools/phmm_probe.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/phmm_f64wg_$T.log || exit 1
