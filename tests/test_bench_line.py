@@ -12,8 +12,8 @@ import bench  # noqa: E402
 
 
 def _record():
-    # a full record in the shape bench.py's main() assembles (last round's real line)
-    with open(os.path.join(ROOT, "profiles", "r03zc_bench.json")) as f:
+    # a full record as bench.py writes it to --detail-out (this round's checkpoint)
+    with open(os.path.join(ROOT, "profiles", "r04m_bench_detail.json")) as f:
         d = json.load(f)
     bench.add_per_core(d, 256, 128)
     return d
