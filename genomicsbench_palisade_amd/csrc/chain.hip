@@ -590,6 +590,7 @@ int batch_new(gb_chain_batch **out) {
     if (e == hipSuccess) e = hipEventCreate(&ev);
   for (auto &ev : B->fj)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&B->fail_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&B->d_vis, sizeof(unsigned long long));
   if (e != hipSuccess) {
     gb::set_error("gb_chain: %s", hipGetErrorString(e));
@@ -708,6 +709,8 @@ int gb_chain_batch_destroy(gb_chain_batch *B) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : B->fj)
     if (ev) (void)hipEventDestroy(ev);
+  if (B->fail_ev) (void)hipEventDestroy(B->fail_ev);
+  if (B->h_fail) (void)hipHostFree(B->h_fail);
   if (B->stream2) (void)hipStreamDestroy(B->stream2);
   if (B->stream) (void)hipStreamDestroy(B->stream);
   delete B;

@@ -90,6 +90,9 @@ struct gb_chain_batch {
   int64_t cap_split = 0, cap_segs = 0, cap_chunks = 0, cap_st = 0, cap_sscore = 0, cap_sparent = 0, cap_smark = 0, cap_need = 0, cap_slow = 0, cap_front = 0,
           cap_jump = 0, cap_t2 = 0, cap_viscall = 0;
   int64_t spec_rounds = 0, fixups = 0;  // statistics of the last run
+  int32_t *h_fail = nullptr;   // pinned copy of d_fail (the host reads it mid-step)
+  int64_t cap_hfail = 0;
+  hipEvent_t fail_ev = nullptr;  // recorded behind the d_fail copy
 };
 
 namespace gbchain {

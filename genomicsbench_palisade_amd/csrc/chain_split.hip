@@ -790,7 +790,15 @@ int split_resolve(gb_chain_batch *B) {
   gb::Range range_("gb.chain.split_resolve");
   const int64_t ns = (int64_t)B->split.size();
   const unsigned nch = (unsigned)B->chunks.size();
-  std::vector<int32_t> front((size_t)ns), fail((size_t)ns);
+  std::vector<int32_t> front((size_t)ns);
+  if (ns > B->cap_hfail) {
+    if (B->h_fail) (void)hipHostFree(B->h_fail);
+    B->h_fail = nullptr;
+    B->cap_hfail = 0;
+    GB_HIP(hipHostMalloc((void **)&B->h_fail, (size_t)ns * sizeof(int32_t), hipHostMallocDefault));
+    B->cap_hfail = ns;
+  }
+  const int32_t *fail = B->h_fail;
   for (int64_t k = 0; k < ns; k++) front[(size_t)k] = B->split[(size_t)k].c1;
   GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
   GB_HIP(hipMemsetAsync(B->d_t2, 0, (size_t)B->nanchors * 4, B->stream));
@@ -807,6 +815,16 @@ int split_resolve(gb_chain_batch *B) {
   std::vector<uint8_t> failed((size_t)ns, 0);
   B->spec_rounds = 0;
   B->fixups = 0;
+  // the peak pass (4.) reads only scores, parents and segment-0 peaks, so it is queued right behind
+  // the first verification, before the host has seen whether any segment failed: the GPU runs it
+  // while the failure flags come back (the common case: none, and the pass is final). A failure
+  // makes it run again at the end; peak_write overwrites every split anchor's peak and target.
+  auto peak_pass = [&]() {
+    hipLaunchKernelGGL(peak_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
+    const int r = jump(B, 1, rounds);
+    hipLaunchKernelGGL(peak_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+  };
+  bool peaks_final = false;
   while (true) {
     B->spec_rounds++;
     hipLaunchKernelGGL(guess_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
@@ -821,8 +839,13 @@ int split_resolve(gb_chain_batch *B) {
       hipLaunchKernelGGL(verify_kernel<true>, dim3(nch), dim3(64), 0, B->stream, A, (const uint64_t *)nullptr);
     }
     GB_HIP(hipGetLastError());
-    GB_HIP(hipMemcpyAsync(fail.data(), B->d_fail, (size_t)ns * 4, hipMemcpyDeviceToHost, B->stream));
-    GB_HIP(hipStreamSynchronize(B->stream));
+    GB_HIP(hipMemcpyAsync(B->h_fail, B->d_fail, (size_t)ns * 4, hipMemcpyDeviceToHost, B->stream));
+    GB_HIP(hipEventRecord(B->fail_ev, B->stream));
+    if (B->spec_rounds == 1) {
+      peak_pass();
+      peaks_final = true;
+    }
+    GB_HIP(hipEventSynchronize(B->fail_ev));  // the failure flags; the peak pass runs on meanwhile
     fix.clear();
     for (int64_t k = 0; k < ns; k++) {
       const int32_t f = fail[(size_t)k];
@@ -838,6 +861,7 @@ int split_resolve(gb_chain_batch *B) {
       front[(size_t)k] = e;
     }
     if (fix.empty()) break;
+    peaks_final = false;
     B->fixups += (int64_t)fix.size();
     // fix-up blocks go behind the block table (split_plan left room for one per split call)
     VCall *d_fix = B->d_vc + B->vc.size();
@@ -868,9 +892,7 @@ int split_resolve(gb_chain_batch *B) {
     }
     GB_HIP(hipStreamSynchronize(B->stream));  // `front` is a host vector about to go
   }
-  hipLaunchKernelGGL(peak_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
-  const int r = jump(B, 1, rounds);
-  hipLaunchKernelGGL(peak_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
+  if (!peaks_final) peak_pass();
   hipLaunchKernelGGL(merge_targets, dim3((unsigned)ns), dim3(256), 0, B->stream, A);
   GB_HIP(hipGetLastError());
   return GB_OK;

@@ -4,6 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=r04l
-PROBE_VARIANTS="base:;wg12:GB_PHMM_F64_WG=12;wg17:GB_PHMM_F64_WG=17;wg20:GB_PHMM_F64_WG=20;wg24:GB_PHMM_F64_WG=24;wg32:GB_PHMM_F64_WG=32" \
-  timeout -k 10 300 python3 tools/phmm_probe.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/phmm_f64wg_$T.log || exit 1
+T=r04n
+CHAIN_SETS=shard0/8 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl_shard_$T -o run -- python3 tools/chain_knob_probe.py > gpurun_out/tl_shard_$T.log 2>&1 || { tail gpurun_out/tl_shard_$T.log; exit 1; }
+python3 tools/kernel_timeline.py gpurun_out/tl_shard_$T chain_rows > gpurun_out/chain_shard_timeline_$T.txt
+tail -45 gpurun_out/chain_shard_timeline_$T.txt
