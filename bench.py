@@ -53,21 +53,57 @@ BSW_OPS_PER_CELL = 13                # ~13 int ops per scalar in
 PEAK_INT_OPS = PEAK_F32_OPS          # 32-bit integer VALU lane-ops/s = 78.6e12
 
 
-def source_digest() -> str:
-    """sha256 (16 hex) of the kernel sources (csrc/ and include/): tools/pmc_summary.py stamps it into
-    each profiles/*_pmc.json, and a bench line's traffic_detail says whether its counters were taken
-    on the code being measured ("stale": false) or on other code (true; null for a file without it)."""
+# kernel sources per leg (file-name prefixes under csrc/ and include/), for the PMC staleness mark
+LEG_SOURCES = {"phmm": ("phmm", "gb_phmm", "gkl"), "fmi": ("fmi", "gb_fmi", "FMI_search"),
+               "chain": ("chain", "gb_chain", "minimap2_chain"), "bsw": ("bsw", "gb_bsw", "bandedSWA")}
+KERNEL_LEG = {"phmm_forward<float>": "phmm", "phmm_forward<double>": "phmm", "smem_search": "fmi",
+              "smem_heavy": "fmi", "sa_walk": "fmi", "chain_rows": "chain", "chain_kernel": "chain",
+              "verify_lanes": "chain", "bsw_lane_kernel": "bsw", "bsw_extend_kernel": "bsw"}
+
+
+def source_files():
     import glob
+    return sorted(glob.glob(os.path.join(ROOT, "genomicsbench_palisade_amd", "csrc", "*"))
+                  + glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*", "*.h")))
+
+
+def digest_of(named):
+    """sha256 (16 hex) over (relative name, bytes) pairs of .hip / .cpp / .h sources, in name order.
+    With a leg, only that leg's sources (LEG_SOURCES) and the shared ones (gb_common*, gb.h)."""
     import hashlib
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "genomicsbench_palisade_amd", "csrc", "*"))
-                   + glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*", "*.h")))
-    for f in files:
-        if f.endswith((".hip", ".cpp", ".h")):
-            h.update(os.path.relpath(f, ROOT).encode())
-            with open(f, "rb") as fh:
-                h.update(fh.read())
+    for rel, data in sorted(named):
+        if rel.endswith((".hip", ".cpp", ".h")):
+            h.update(rel.encode())
+            h.update(data)
     return h.hexdigest()[:16]
+
+
+def _leg_match(rel, leg):
+    b = os.path.basename(rel)
+    return leg is None or b.startswith(LEG_SOURCES[leg]) or b.startswith(("gb_common", "gb.h"))
+
+
+def source_digest(leg=None) -> str:
+    """Digest of the kernel sources (csrc/ and include/), or of one leg's: tools/pmc_summary.py
+    stamps them into each profiles/*_pmc.json, and a bench line's traffic_detail says whether its
+    counters were taken on the kernel code being measured ("stale": false) or on other code (true;
+    null for a file without a stamp)."""
+    named = []
+    for f in source_files():
+        rel = os.path.relpath(f, ROOT)
+        if _leg_match(rel, leg):
+            with open(f, "rb") as fh:
+                named.append((rel, fh.read()))
+    return digest_of(named)
+
+
+def _stale(d, kernel):
+    leg = KERNEL_LEG.get(kernel)
+    legs = d.get("_code_legs") or {}
+    if leg and leg in legs:
+        return legs[leg] != source_digest(leg)
+    return (d["_code"] != source_digest()) if "_code" in d else None
 
 
 def pmc_traffic_detail(kernel: str, leg: str = ""):
@@ -98,7 +134,7 @@ def pmc_traffic_detail(kernel: str, leg: str = ""):
                     "fetch_bytes_raw": k["fetch_bytes_raw"], "fetch_factor": k["fetch_factor"],
                     "fetch_class": k["fetch_class"], "write_bytes": k["write_bytes"],
                     "source": os.path.relpath(f, ROOT),
-                    "stale": (d["_code"] != source_digest()) if "_code" in d else None}
+                    "stale": _stale(d, kernel)}
     return None
 
 

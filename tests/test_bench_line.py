@@ -81,3 +81,28 @@ def test_pmc_traffic_marks_other_code_stale(tmp_path, monkeypatch):
 def test_source_digest_is_stable():
     assert bench.source_digest() == bench.source_digest()
     assert len(bench.source_digest()) == 16
+
+
+def test_pmc_staleness_is_per_leg(tmp_path, monkeypatch):
+    # a file stamped per leg: a kernel is stale only when its own leg's sources changed
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"fetch_bytes": 2.0, "fetch_bytes_raw": 1.0, "fetch_factor": 2.0, "fetch_class": "stream",
+             "write_bytes": 1.0}
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "source_digest", lambda leg=None: {"chain": "new"}.get(leg, "same"))
+    (prof / "r09a_pmc.json").write_text(json.dumps({
+        "chain_rows": entry, "phmm_forward<float>": entry, "_code": "old",
+        "_code_legs": {"phmm": "same", "fmi": "same", "chain": "old", "bsw": "same"}}))
+    assert bench.pmc_traffic_detail("chain_rows")["stale"] is True
+    assert bench.pmc_traffic_detail("phmm_forward<float>")["stale"] is False
+
+
+def test_leg_sources_cover_every_kernel_file():
+    # every kernel source belongs to one leg or is shared, so no change escapes the staleness mark
+    for f in bench.source_files():
+        rel = os.path.relpath(f, bench.ROOT)
+        b = os.path.basename(rel)
+        if not rel.endswith((".hip", ".cpp", ".h")) or b.startswith(("gb_common", "gb.h")):
+            continue
+        assert sum(b.startswith(p) for p in bench.LEG_SOURCES.values()) == 1, rel

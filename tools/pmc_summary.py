@@ -88,8 +88,9 @@ def main():
                   "fetch_class": cls, "fetch_factor": FETCH_FACTOR[cls],
                   "write_bytes": sum(wb) / max(len(wb), 1), "mean_ms_under_pmc": sum(ms) / max(len(ms), 1)}
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from bench import source_digest
-    res["_code"] = source_digest()  # bench.py marks traffic from other code "stale"
+    from bench import LEG_SOURCES, source_digest
+    res["_code"] = source_digest()  # bench.py marks traffic from other kernel code "stale"
+    res["_code_legs"] = {leg: source_digest(leg) for leg in LEG_SOURCES}
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch; fetch "
                     "scaled by the calibrated factor of the kernel's read class (tools/probes/pmc_calib.hip, "
                     "profiles/r01g_pmc_calib.txt), write exact")
