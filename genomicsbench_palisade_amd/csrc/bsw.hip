@@ -670,10 +670,16 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // per pair: descriptor, kernel variant and sort key -- in parallel chunks for big batches; a bad
   // pair is reported by the sequential check below (first offending index)
   // variant: the pair-per-lane kernel needs qlen < 8*NCH (NCH <= 20) and scores that fit the 16-bit
-  // eh packing; everything else goes to the wave-per-pair kernel. Sort key: variant, then query
-  // length in steps of 4 (similar band ends per wave), then decreasing target length (similar row
-  // counts per wave).
+  // eh packing; everything else goes to the wave-per-pair kernel. Sort key: variant, then whether
+  // h0 is 0, then query length in steps of 4 (similar band ends per wave), then decreasing target
+  // length (similar row counts per wave). A pair with h0 = 0 ends after its first row (every H of
+  // row 0 is 0, so its row maximum is 0, bandedSWA.cpp:222-223): mixed into a wave it leaves its lane
+  // idle for the wave's whole run, so those pairs get waves of their own.
   constexpr int kQB = 64, kTB = 4096;
+  auto sort_key = [](int v, const gbbsw::Pair &q) {
+    return (uint32_t)((((size_t)v * 2 + (q.h0 == 0 ? 1 : 0)) * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
+                      (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1)));
+  };
   const bool lane_ok = params->o_del >= 0 && params->o_ins >= 0 && mn >= -128 && mx <= 127;
   std::vector<gbbsw::Pair> P((size_t)n);
   std::vector<uint8_t> var((size_t)n);
@@ -697,8 +703,7 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
         v = nch <= 4 ? 0 : nch <= 8 ? 1 : nch <= 12 ? 2 : nch <= 16 ? 3 : nch <= 20 ? 4 : 5;
       }
       var[p] = (uint8_t)v;
-      keys[p] = (uint32_t)(((size_t)v * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
-                           (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1)));
+      keys[p] = sort_key(v, q);
     }
   };
   const int nth = n >= (1 << 17) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
@@ -731,16 +736,15 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
       std::vector<uint32_t> cost;
       cost.reserve((size_t)n);
       for (int64_t p = 0; p < n; ++p)
-        if (var[p] < 5) cost.push_back((uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)));
+        if (var[p] < 5 && P[p].h0 != 0) cost.push_back((uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)));
       const size_t k = (size_t)((double)cost.size() * frac);
       if (k > 0 && k < cost.size()) {
         std::nth_element(cost.begin(), cost.end() - (ptrdiff_t)k, cost.end());
         const uint32_t cut = *(cost.end() - (ptrdiff_t)k);
         for (int64_t p = 0; p < n; ++p)
-          if (var[p] < 5 && (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)) >= cut) {
+          if (var[p] < 5 && P[p].h0 != 0 && (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)) >= cut) {
             var[p] = 5;
-            keys[p] = (uint32_t)(((size_t)5 * kQB + (size_t)(kQB - 1 - std::min(P[p].qlen >> 2, kQB - 1))) * kTB +
-                                 (size_t)(kTB - 1 - std::min(P[p].tlen, kTB - 1)));
+            keys[p] = sort_key(5, P[p]);
           }
       }
     }
@@ -752,7 +756,7 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     for (int64_t p = 0; p < n; ++p) order[(size_t)p] = (uint32_t)p;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
   } else {
-    std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * kQB * kTB + 1, 0);
+    std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * 2 * kQB * kTB + 1, 0);
     for (int64_t p = 0; p < n; ++p) cnt[keys[p]]++;
     int64_t acc = 0;
     for (auto &c : cnt) {

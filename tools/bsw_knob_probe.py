@@ -11,6 +11,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import genomicsbench_palisade_amd as g  # noqa: E402
+if os.environ.get("BSW_LIB"):  # another build of libgb.so, to time two builds on one box
+    g.LIBGB = os.path.abspath(os.environ["BSW_LIB"])
 from genomicsbench_palisade_amd import bsw, gen, set_device, shard  # noqa: E402
 
 KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL")
@@ -42,5 +45,5 @@ for name, ps in sets:
         if base is None:
             base = (out6, cells)
         same = np.array_equal(out6, base[0]) and np.array_equal(cells, base[1])
-        print(f"{name:8s} [{cfg or 'default':32s}] {best:8.3f} ms  {tot / best / 1e6:8.1f} GCUPS  same={same}", flush=True)
+        print(f"{os.path.basename(g.LIBGB)} {name:8s} [{cfg or 'default':32s}] {best:8.3f} ms  {tot / best / 1e6:8.1f} GCUPS  same={same}", flush=True)
     b.close()
