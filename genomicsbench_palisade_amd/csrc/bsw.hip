@@ -675,11 +675,19 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // length (similar row counts per wave). A pair with h0 = 0 ends after its first row (every H of
   // row 0 is 0, so its row maximum is 0, bandedSWA.cpp:222-223): mixed into a wave it leaves its lane
   // idle for the wave's whole run, so those pairs get waves of their own.
-  constexpr int kQB = 64, kTB = 4096;
-  auto sort_key = [](int v, const gbbsw::Pair &q) {
-    return (uint32_t)((((size_t)v * 2 + (q.h0 == 0 ? 1 : 0)) * kQB + (size_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1))) * kTB +
-                      (size_t)(kTB - 1 - std::min(q.tlen, kTB - 1)));
+  // The key is (high, low): high = variant, h0 == 0, query length in steps of 4 (similar band ends
+  // per wave), h0 in steps of 10 (the first rows' band of nonzero cells is ~h0 - o_ins wide, so it
+  // sets how far the early rows sweep); low = decreasing target length (similar row counts).
+  constexpr int kQB = 64, kHB = 8, kTB = 4096;
+  const char *ke = getenv("GB_BSW_H0STEP");  // probes: the h0 step (0: h0 not in the key)
+  const int h0step = ke ? atoi(ke) : 10;
+  auto key_hi = [h0step](int v, const gbbsw::Pair &q) {
+    const uint32_t z = q.h0 == 0 ? 1 : 0, qb = (uint32_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1));
+    const uint32_t hb = h0step > 0 ? (uint32_t)std::min(std::max(q.h0, 0) / h0step, kHB - 1) : 0;
+    return (((uint32_t)v * 2 + z) * kQB + qb) * kHB + hb;
   };
+  auto key_lo = [](const gbbsw::Pair &q) { return (uint32_t)(kTB - 1 - std::min(q.tlen, kTB - 1)); };
+  auto sort_key = [&](int v, const gbbsw::Pair &q) { return key_hi(v, q) * (uint32_t)kTB + key_lo(q); };
   const bool lane_ok = params->o_del >= 0 && params->o_ins >= 0 && mn >= -128 && mx <= 127;
   std::vector<gbbsw::Pair> P((size_t)n);
   std::vector<uint8_t> var((size_t)n);
@@ -756,15 +764,30 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     for (int64_t p = 0; p < n; ++p) order[(size_t)p] = (uint32_t)p;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
   } else {
-    std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * 2 * kQB * kTB + 1, 0);
-    for (int64_t p = 0; p < n; ++p) cnt[keys[p]]++;
-    int64_t acc = 0;
-    for (auto &c : cnt) {
-      const int64_t t = c;
-      c = acc;
-      acc += t;
+    // two stable counting passes (least significant first): by the low key, then the high key
+    std::vector<uint32_t> tmp((size_t)n);
+    {
+      std::vector<int64_t> cnt((size_t)kTB + 1, 0);
+      for (int64_t p = 0; p < n; ++p) cnt[keys[p] % kTB]++;
+      int64_t acc = 0;
+      for (auto &c : cnt) {
+        const int64_t t = c;
+        c = acc;
+        acc += t;
+      }
+      for (int64_t p = 0; p < n; ++p) tmp[cnt[keys[p] % kTB]++] = (uint32_t)p;
     }
-    for (int64_t p = 0; p < n; ++p) order[cnt[keys[p]]++] = (uint32_t)p;
+    {
+      std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * 2 * kQB * kHB + 1, 0);
+      for (int64_t p = 0; p < n; ++p) cnt[keys[p] / kTB]++;
+      int64_t acc = 0;
+      for (auto &c : cnt) {
+        const int64_t t = c;
+        c = acc;
+        acc += t;
+      }
+      for (int64_t k = 0; k < n; ++k) order[cnt[keys[tmp[k]] / kTB]++] = tmp[k];
+    }
   }
   for (int v = 0; v <= gb_bsw_batch::kVariants; ++v) B->seg[v] = 0;
   for (int64_t p = 0; p < n; ++p) B->seg[var[p] + 1]++;

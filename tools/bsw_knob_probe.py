@@ -16,7 +16,7 @@ if os.environ.get("BSW_LIB"):  # another build of libgb.so, to time two builds o
     g.LIBGB = os.path.abspath(os.environ["BSW_LIB"])
 from genomicsbench_palisade_amd import bsw, gen, set_device, shard  # noqa: E402
 
-KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL")
+KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP")
 set_device(0)
 pairs = gen.bsw_dataset(seed=11, threads=16)
 sets = [("large", pairs)]
@@ -34,6 +34,9 @@ for name, ps in sets:
         for kv in [c for c in cfg.split("+") if c]:
             k, v = kv.split("=", 1)
             os.environ[k] = v
+        if os.environ.get("BSW_REBUILD") == "1":  # knobs read when a batch is made (GB_BSW_KEY)
+            b.close()
+            b = bsw.BswBatch(ps)
         b.run()
         b.sync()
         best = 1e9

@@ -4,6 +4,8 @@
 #   smoke  __graft_entry__.smoke()
 #   bench  the driver's command           -> gpurun_out/bench_TAG.json (headline) + bench_TAG_detail.json
 #   prof   kernel-trace stats + FETCH/WRITE PMC passes (tools/gpu_prof.sh)
+#   pmcsum those passes summarised into profiles/TAG_pmc.json on the box (run before bench, so the
+#          bench line's traffic is this checkpoint's)
 #   lds    LDS-conflict / VALU-busy SQ counters per leg (tools/gpu_lds.sh)
 # Usage: gpu_checkpoint.sh TAG [stages...]   (default stages: tests smoke bench)
 #   gpurun --timeout 1200 -- 'bash tools/gpu_checkpoint.sh r04a tests smoke bench prof'
@@ -34,6 +36,19 @@ for s in $STAGES; do
       [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_${TAG}.err; exit 1; } ;;
     prof)
       bash tools/gpu_prof.sh ${TAG} || exit 1 ;;
+    pmcsum)
+      # the prof stage's PMC passes summarised into profiles/ on the box, so a bench stage after it
+      # cites this checkpoint's traffic (copies come back under gpurun_out/ for collect_checkpoint)
+      for pre in pmc pmch; do
+        fd=$(find gpurun_out/${pre}_fetch_${TAG} -name run_counter_collection.csv | sort | tail -1)
+        wd=$(find gpurun_out/${pre}_write_${TAG} -name run_counter_collection.csv | sort | tail -1)
+        [ -n "$fd" ] && [ -n "$wd" ] || { echo "pmcsum: no ${pre} passes for ${TAG}"; exit 1; }
+        dst=profiles/${TAG}_pmc.json
+        [ $pre = pmch ] && dst=profiles/${TAG}_human_pmc.json
+        python3 tools/pmc_summary.py "$(dirname "$fd")" "$(dirname "$wd")" $dst > /dev/null || exit 1
+        cp $dst gpurun_out/pmcsum_$(basename $dst)
+      done
+      echo "pmcsum ok" ;;
     lds)
       bash tools/gpu_lds.sh ${TAG} || exit 1 ;;
     *)
