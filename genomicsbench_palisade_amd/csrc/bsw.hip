@@ -765,7 +765,8 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
   } else {
     // two stable counting passes (least significant first): by the low key, then the high key
-    std::vector<uint32_t> tmp((size_t)n);
+    // (the first pass carries each pair's high key along, so the second reads it sequentially)
+    std::vector<uint32_t> tmp((size_t)n), thi((size_t)n);
     {
       std::vector<int64_t> cnt((size_t)kTB + 1, 0);
       for (int64_t p = 0; p < n; ++p) cnt[keys[p] % kTB]++;
@@ -775,18 +776,22 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
         c = acc;
         acc += t;
       }
-      for (int64_t p = 0; p < n; ++p) tmp[cnt[keys[p] % kTB]++] = (uint32_t)p;
+      for (int64_t p = 0; p < n; ++p) {
+        const int64_t at = cnt[keys[p] % kTB]++;
+        tmp[(size_t)at] = (uint32_t)p;
+        thi[(size_t)at] = keys[p] / kTB;
+      }
     }
     {
       std::vector<int64_t> cnt((size_t)gb_bsw_batch::kVariants * 2 * kQB * kHB + 1, 0);
-      for (int64_t p = 0; p < n; ++p) cnt[keys[p] / kTB]++;
+      for (int64_t k = 0; k < n; ++k) cnt[thi[k]]++;
       int64_t acc = 0;
       for (auto &c : cnt) {
         const int64_t t = c;
         c = acc;
         acc += t;
       }
-      for (int64_t k = 0; k < n; ++k) order[cnt[keys[tmp[k]] / kTB]++] = tmp[k];
+      for (int64_t k = 0; k < n; ++k) order[cnt[thi[k]]++] = tmp[k];
     }
   }
   for (int v = 0; v <= gb_bsw_batch::kVariants; ++v) B->seg[v] = 0;
