@@ -394,6 +394,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
     uint32_t nz[NW];
 #pragma unroll
     for (int q = 0; q < NW; ++q) nz[q] = 0;
+    // the lane's band [beg, beg + width) as a bitmap, one word per 32 columns: a column's select mask
+    // is then one sign-extending bit extract (the compare of j - beg against width was two ops)
+    uint32_t bw[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int lo = min(max(beg - 32 * q, 0), 32), hi = min(max(beg + width - 32 * q, 0), 32);
+      const int nb = hi - lo;
+      bw[q] = nb > 0 ? (0xFFFFFFFFu >> (32 - nb)) << lo : 0u;
+    }
     uint32_t qn = Qs[0][lane];
     // chunks meeting some lane's band: the OR of every lane's chunk range [beg >> 3, (end - 1) >> 3]
     const uint32_t swm = wave_or(width > 0 ? (2u << ((end - 1) >> 3)) - (1u << (beg >> 3)) : 0u);
@@ -416,7 +425,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
       for (int b = 0; b < 8; ++b) {
         const int j = 8 * c + b;
         // lane mask of the band, used as a bit-select (kept arithmetic so no branches come back)
-        const uint32_t msk = (uint32_t)(j - beg) < (uint32_t)width ? 0xFFFFFFFFu : 0u;
+        uint32_t msk;  // bit j of the band bitmap, sign-extended (asm: the compiler turns the shift form
+                       // back into an AND and a compare)
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(msk) : "v"(bw[j >> 5]), "i"(j & 31));
         const uint32_t x = X[j];
         const int sb = (int)(int8_t)(((b & 1) ? so : se) >> (8 * (b >> 1)));  // score, sign-extended
         const int y = (int)(x >> 16) + sb;                                    // H + S
@@ -429,7 +440,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         // the full rate, a v_lshl_or at 4.27 cycles); en, h1 < 2^16
         uint32_t xn = (uint32_t)en;
         asm("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0" : "+v"(xn) : "v"(h1));
-        nz[j >> 5] |= (min(xn, 1u) & msk) << (j & 31);
+        uint32_t nzb;  // xn != 0 as 0 / 1 (asm: kept out of the compiler's compare-and-select form)
+        asm("v_min_u32 %0, %1, 1" : "=v"(nzb) : "v"(xn));
+        nz[j >> 5] |= nzb << (j & 31);  // out-of-band bits are cleared after the sweep
         X[j] = (xn & msk) | (x & ~msk);
         f = (int)(((uint32_t)fn & msk) | ((uint32_t)f & ~msk));
         h1 = (int)(((uint32_t)h & msk) | ((uint32_t)h1 & ~msk));
@@ -438,6 +451,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         mkey = max(mkey, (int)((uint32_t)h1 << 8 | (uint32_t)j));
       }
     }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) nz[q] &= bw[q];
     // eh[end] = {h1, 0} (bandedSWA.cpp:217), chunks holding no lane's end skipped
     const bool wend = active && end < NCOL;
     // chunks holding some lane's end: one wave OR of one-hot chunk bits (DPP row shifts + row
