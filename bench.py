@@ -64,7 +64,8 @@ KERNEL_LEG = {"phmm_forward<float>": "phmm", "phmm_forward<double>": "phmm", "sm
 def source_files():
     import glob
     return sorted(glob.glob(os.path.join(ROOT, "genomicsbench_palisade_amd", "csrc", "*"))
-                  + glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*", "*.h")))
+                  + glob.glob(os.path.join(ROOT, "include", "*.h")) + glob.glob(os.path.join(ROOT, "include", "*", "*.h"))
+                  + [os.path.join(ROOT, "Makefile")])  # build flags shape the kernels too
 
 
 def digest_of(named):
@@ -73,7 +74,7 @@ def digest_of(named):
     import hashlib
     h = hashlib.sha256()
     for rel, data in sorted(named):
-        if rel.endswith((".hip", ".cpp", ".h")):
+        if rel.endswith((".hip", ".cpp", ".h")) or os.path.basename(rel) == "Makefile":
             h.update(rel.encode())
             h.update(data)
     return h.hexdigest()[:16]
@@ -81,7 +82,7 @@ def digest_of(named):
 
 def _leg_match(rel, leg):
     b = os.path.basename(rel)
-    return leg is None or b.startswith(LEG_SOURCES[leg]) or b.startswith(("gb_common", "gb.h"))
+    return leg is None or b.startswith(LEG_SOURCES[leg]) or b.startswith(("gb_common", "gb.h")) or b == "Makefile"
 
 
 def source_digest(leg=None) -> str:

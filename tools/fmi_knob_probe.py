@@ -9,6 +9,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import genomicsbench_palisade_amd as g  # noqa: E402
+if os.environ.get("FMI_LIB"):  # another build of libgb.so, to time two builds on one box
+    g.LIBGB = os.path.abspath(os.environ["FMI_LIB"])
 from genomicsbench_palisade_amd import fmi, gen, set_device, shard  # noqa: E402
 
 KNOBS = ("GB_FMI_WAVES_PER_CU", "GB_FMI_TOP", "GB_FMI_HEAVY", "GB_FMI_QLDS", "GB_FMI_PREFETCH")
@@ -39,7 +42,7 @@ for name, (a, b) in (("full", (0, nreads)), ("shard0/8", (lo, hi))):
             kbest = min(kbest, rs.timing()[0])
         _, tot, _, _ = rs.results(batch_size=512, want_smems=False)
         base = tot if base is None else base
-        print(f"{name:8s} [{cfg or 'default':45s}] wall {best * 1e3:8.2f} ms, search {kbest:8.2f} ms "
+        print(f"{os.path.basename(g.LIBGB)} {name:8s} [{cfg or 'default':45s}] wall {best * 1e3:8.2f} ms, search {kbest:8.2f} ms "
               f"({(b - a) / best / 1e6:6.2f} Mreads/s) smems {tot} same={tot == base}", flush=True)
         rs.close()
 idx.close()

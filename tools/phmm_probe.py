@@ -4,6 +4,9 @@ environment variables (read when a batch runs): PROBE_VARIANTS="NAME:VAR=VAL,VAR
 import os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import genomicsbench_palisade_amd as g  # noqa: E402
+if os.environ.get("PHMM_LIB"):  # another build of libgb.so, to time two builds on one box
+    g.LIBGB = os.path.abspath(os.environ["PHMM_LIB"])
 from genomicsbench_palisade_amd import gen, phmm, set_device
 from genomicsbench_palisade_amd._tc import TestcaseArray
 set_device(0)
@@ -46,5 +49,5 @@ for hm in [int(x) for x in os.environ.get("PHMM_HAPMAX", "473").split(",")]:
                 else:
                     os.environ[k] = v
             a = min(x[0] for x in ts[1:]); b = min(x[1] for x in ts[1:]); t = min(x[2] for x in ts[1:])
-            print(f"hap_max {hm} {name:10s}: f32 {a:.3f} ms ({cells / a / 1e6:.0f} GCUPS f32)  f64 {b:.3f} ms  total {t:.3f} ms -> {cells / t / 1e6:.0f} GCUPS", flush=True)
+            print(f"{os.path.basename(g.LIBGB)} hap_max {hm} {name:10s}: f32 {a:.3f} ms ({cells / a / 1e6:.0f} GCUPS f32)  f64 {b:.3f} ms  total {t:.3f} ms -> {cells / t / 1e6:.0f} GCUPS", flush=True)
     job.close()
