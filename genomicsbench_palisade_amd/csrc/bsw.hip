@@ -458,18 +458,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
     // chunks holding some lane's end: one wave OR of one-hot chunk bits (DPP row shifts + row
     // broadcasts, lane 63 holds the result), then scalar bit tests instead of a ballot per chunk
     const uint32_t endm = wave_or(wend ? 1u << (end >> 3) : 0u);
+    // the lane's end column as a one-bit map per 32-column word: in a chunk holding some lane's end
+    // a column costs a bit extract and a bit-select (a compare, a mask AND and two selects before,
+    // and the compiler hoisted every column's nonzero bit out of the chunk test), and the nonzero
+    // bitmap takes h1's bit at the end column once per word
+    uint32_t ew[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) ew[q] = (wend && (end >> 5) == q) ? 1u << (end & 31) : 0u;
+    const uint32_t h1s = (uint32_t)h1 << 16;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (((endm >> c) & 1u) == 0) continue;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const int j = 8 * c + b;
-        if (wend && end == j) {
-          X[j] = (uint32_t)h1 << 16;
-          nz[j >> 5] = (nz[j >> 5] & ~(1u << (j & 31))) | (min((uint32_t)h1, 1u) << (j & 31));
-        }
+        uint32_t m;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(ew[j >> 5]), "i"(j & 31));
+        X[j] = (h1s & m) | (X[j] & ~m);
       }
     }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) nz[q] = (nz[q] & ~ew[q]) | (h1 ? ew[q] : 0u);
     if (!active) continue;
     // keys past the band end repeat H(end-1) at larger j, so a winner there is column end-1; an
     // empty band computed nothing (row max 0, bandedSWA.cpp:222)
