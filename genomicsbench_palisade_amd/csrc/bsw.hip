@@ -700,13 +700,15 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // row 0 is 0, so its row maximum is 0, bandedSWA.cpp:222-223): mixed into a wave it leaves its lane
   // idle for the wave's whole run, so those pairs get waves of their own.
   // The key is (high, low): high = variant, h0 == 0, query length in steps of 4 (similar band ends
-  // per wave), h0 in steps of 10 (the first rows' band of nonzero cells is ~h0 - o_ins wide, so it
+  // per wave), h0 in steps of 8 (the first rows' band of nonzero cells is ~h0 - o_ins wide, so it
   // sets how far the early rows sweep); low = decreasing target length (similar row counts).
   constexpr int kQB = 64, kHB = 8, kTB = 4096;
   const char *ke = getenv("GB_BSW_H0STEP");  // probes: the h0 step (0: h0 not in the key)
-  const int h0step = ke ? atoi(ke) : 10;
-  auto key_hi = [h0step](int v, const gbbsw::Pair &q) {
-    const uint32_t z = q.h0 == 0 ? 1 : 0, qb = (uint32_t)(kQB - 1 - std::min(q.qlen >> 2, kQB - 1));
+  const int h0step = ke ? atoi(ke) : 8;
+  const char *qe = getenv("GB_BSW_QSHIFT");  // probes: query-length step 1 << QSHIFT (default 4)
+  const int qshift = qe ? std::min(std::max(atoi(qe), 0), 6) : 2;
+  auto key_hi = [h0step, qshift](int v, const gbbsw::Pair &q) {
+    const uint32_t z = q.h0 == 0 ? 1 : 0, qb = (uint32_t)(kQB - 1 - std::min(q.qlen >> qshift, kQB - 1));
     const uint32_t hb = h0step > 0 ? (uint32_t)std::min(std::max(q.h0, 0) / h0step, kHB - 1) : 0;
     return (((uint32_t)v * 2 + z) * kQB + qb) * kHB + hb;
   };
