@@ -122,6 +122,24 @@ def test_gpu_vs_oracle(seed, n, qlen, extra):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("h0step,qshift", [("0", "2"), ("3", "0"), ("8", "6"), ("40", "3")])
+def test_gpu_grouping_key_does_not_change_results(monkeypatch, h0step, qshift):
+    """The batch's sort key (variant, h0 == 0, query length step, h0 step, target length) only orders
+    pairs into waves; every grouping must give the oracle's outputs and cell counts, scattered back to
+    the caller's order (pairs with h0 0, large h0 and every variant in the set)."""
+    monkeypatch.setenv("GB_BSW_H0STEP", h0step)
+    monkeypatch.setenv("GB_BSW_QSHIFT", qshift)
+    p = gen.bsw_pairs(30000, seed=17, qlen=(1, 160), extra=(0, 200))
+    p.h0[::7] = 0
+    p.h0[1::11] = 200
+    P = bsw.default_params()
+    got, cells, tot = _gpu(p, P)
+    exp, ocells, otot = oracle_lib.bsw_oracle(p, P, nthreads=8)
+    assert_same(got, exp, f"h0 step {h0step}, query shift {qshift}")
+    assert (cells == ocells).all() and tot == otot
+
+
+@pytest.mark.gpu
 def test_gpu_get_scores16_and_repeat():
     from genomicsbench_palisade_amd import set_device
     set_device(0)
