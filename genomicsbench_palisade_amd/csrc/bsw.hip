@@ -694,22 +694,23 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // per pair: descriptor, kernel variant and sort key -- in parallel chunks for big batches; a bad
   // pair is reported by the sequential check below (first offending index)
   // variant: the pair-per-lane kernel needs qlen < 8*NCH (NCH <= 20) and scores that fit the 16-bit
-  // eh packing; everything else goes to the wave-per-pair kernel. Sort key: variant, then whether
-  // h0 is 0, then query length in steps of 4 (similar band ends per wave), then decreasing target
-  // length (similar row counts per wave). A pair with h0 = 0 ends after its first row (every H of
-  // row 0 is 0, so its row maximum is 0, bandedSWA.cpp:222-223): mixed into a wave it leaves its lane
-  // idle for the wave's whole run, so those pairs get waves of their own.
-  // The key is (high, low): high = variant, h0 == 0, query length in steps of 4 (similar band ends
-  // per wave), h0 in steps of 8 (the first rows' band of nonzero cells is ~h0 - o_ins wide, so it
-  // sets how far the early rows sweep); low = decreasing target length (similar row counts).
+  // eh packing; everything else goes to the wave-per-pair kernel. A pair with h0 = 0 ends after its
+  // first row (every H of row 0 is 0, so its row maximum is 0, bandedSWA.cpp:222-223): mixed into a
+  // wave it leaves its lane idle for the wave's whole run, so those pairs get waves of their own.
+  // The sort key is (high, low): high = variant, h0 == 0, h0 in steps of 8 (the first rows' band of
+  // nonzero cells is ~h0 - o_ins wide, so it sets how far the early rows sweep), query length in
+  // steps of 8 (similar band ends per wave); low = decreasing target length (similar row counts).
   constexpr int kQB = 64, kHB = 8, kTB = 4096;
   const char *ke = getenv("GB_BSW_H0STEP");  // probes: the h0 step (0: h0 not in the key)
   const int h0step = ke ? atoi(ke) : 8;
-  const char *qe = getenv("GB_BSW_QSHIFT");  // probes: query-length step 1 << QSHIFT (default 4)
-  const int qshift = qe ? std::min(std::max(atoi(qe), 0), 6) : 2;
-  auto key_hi = [h0step, qshift](int v, const gbbsw::Pair &q) {
+  const char *qe = getenv("GB_BSW_QSHIFT");  // probes: query-length step 1 << QSHIFT (default 8)
+  const int qshift = qe ? std::min(std::max(atoi(qe), 0), 6) : 3;
+  const char *oe = getenv("GB_BSW_KEYORD");  // probes: 0 = query length before the h0 step
+  const bool h0first = !(oe && atoi(oe) == 0);
+  auto key_hi = [h0step, qshift, h0first](int v, const gbbsw::Pair &q) {
     const uint32_t z = q.h0 == 0 ? 1 : 0, qb = (uint32_t)(kQB - 1 - std::min(q.qlen >> qshift, kQB - 1));
     const uint32_t hb = h0step > 0 ? (uint32_t)std::min(std::max(q.h0, 0) / h0step, kHB - 1) : 0;
+    if (h0first) return (((uint32_t)v * 2 + z) * kHB + hb) * kQB + qb;
     return (((uint32_t)v * 2 + z) * kQB + qb) * kHB + hb;
   };
   auto key_lo = [](const gbbsw::Pair &q) { return (uint32_t)(kTB - 1 - std::min(q.tlen, kTB - 1)); };

@@ -16,7 +16,7 @@ if os.environ.get("BSW_LIB"):  # another build of libgb.so, to time two builds o
     g.LIBGB = os.path.abspath(os.environ["BSW_LIB"])
 from genomicsbench_palisade_amd import bsw, gen, set_device, shard  # noqa: E402
 
-KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP", "GB_BSW_QSHIFT")
+KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP", "GB_BSW_QSHIFT", "GB_BSW_KEYORD")
 set_device(0)
 pairs = gen.bsw_dataset(seed=11, threads=16)
 sets = [("large", pairs)]
