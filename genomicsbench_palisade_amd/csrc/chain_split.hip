@@ -43,7 +43,11 @@
 namespace gbchain {
 
 constexpr int kSegDefault = 4096;   // longest segment
-constexpr int kWarmDefault = 128;   // warm-up anchors before the window of a segment's first anchor
+// warm-up anchors before the window of a segment's first anchor. Measured (tools/chain_knob_probe.py,
+// profiles/r04zj_chain_warm_ab.log): 128 -> 32 takes the 1/8 shard from 1.47 to 1.37 ms and 'large'
+// from 5.09 to 5.06 ms; 16 and 8 also guess right on both sets, 0 fails (3 fix-ups, shard 2.16 ms),
+// so 32 keeps a margin for sets whose loops reach further back
+constexpr int kWarmDefault = 32;
 // A segment's block starts kWarm anchors before the window of its first anchor, but at most kWinCap
 // anchors of that window: the window is every anchor within max_dist_x (up to max_iter = 5000 in
 // dense regions, median ~500 on the bench's sets) while the reference loop stops after ~30
