@@ -20,17 +20,18 @@ HDRS := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 .PHONY: all ref clean oracle
 DROPINS := $(LIB)/libgkl_pairhmm_c.so $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so $(LIB)/libgb_fmi_dropin.so
 all: $(LIB)/libgb.so $(DROPINS) $(BIN)/phmm $(BIN)/chain $(BIN)/bsw $(BIN)/fmi oracle tests/_build/fmi_class_driver \
-     tests/_build/libdropin_bench.so
+     tests/_build/libdropin_bench.so tests/_build/liblds_poison.so
 
 # the latency-bound DP loops schedule better for instruction-level parallelism (chain_rows -1.8 %,
 # phmm +0.8 %, bsw / fmi neutral; profiles/r04zb_sched_ab.log)
 $(LIB)/obj/chain_rows.o $(LIB)/obj/phmm.o: HIPFLAGS += -mllvm -amdgpu-sched-strategy=max-ilp
 
-$(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS)
+# the Makefile itself is a prerequisite: flag changes (the per-object scheduler flags above) rebuild
+$(LIB)/obj/%.o: $(CSRC)/%.hip $(HDRS) Makefile
 	@mkdir -p $(LIB)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB)/obj/gb_common.o: $(CSRC)/gb_common.cpp $(HDRS)
+$(LIB)/obj/gb_common.o: $(CSRC)/gb_common.cpp $(HDRS) Makefile
 	@mkdir -p $(LIB)/obj
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -71,6 +72,11 @@ tests/_build/fmi_class_driver: tests/cpp/fmi_class_driver.cpp $(LIB)/libgb_fmi_d
 tests/_build/libdropin_bench.so: tests/cpp/dropin_bench.cpp $(LIB)/libgb_chain_dropin.so $(LIB)/libgb_bsw_dropin.so $(wildcard include/gb_compat/*.h)
 	@mkdir -p tests/_build
 	$(HOSTCXX) $(HOSTFLAGS) -pthread -shared -o $@ $< -L$(LIB) -lgb_chain_dropin -lgb_bsw_dropin -lgb -Wl,-rpath,'$$ORIGIN/../../$(LIB)'
+
+# test infrastructure: fills every CU's LDS with adversarial patterns (tests/test_lds_poison.py)
+tests/_build/liblds_poison.so: tests/cpp/lds_poison.hip
+	@mkdir -p tests/_build
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -shared -o $@ $<
 
 oracle:
 	$(MAKE) -s -C oracle all

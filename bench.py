@@ -433,6 +433,8 @@ def _leg_short(leg):
         out["workload"] = re.sub(r" \([^)]*\)", "", wl.split(";")[0])[:100]
     out["roofline"] = _roof_short(leg.get("roofline"))
     out["cpu_baseline"] = _cpu_short(leg.get("cpu_baseline"))
+    if isinstance(leg.get("split_stats"), dict):
+        out["fixups"] = leg["split_stats"].get("fixup_blocks")
     sp = leg.get("shard_proxy")
     if isinstance(sp, dict):
         out["shard_proxy"] = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
@@ -472,6 +474,16 @@ def headline(line: dict, detail_path=None) -> dict:
         h["fmi"]["human"]["rows"] = (hu.get("config") or {}).get("workload", "").split("BWT rows ")[-1].split(",")[0]
     if isinstance(line.get("small"), dict):
         h["small"] = {k: _sig(v.get("value")) for k, v in line["small"].items() if isinstance(v, dict)}
+    # world > 1: gathered shard outputs vs a 1-rank pass of the whole set, per leg (rank_check)
+    rc = {"phmm": line.get("rank_check")}
+    for leg in ("fmi", "chain", "bsw"):
+        rc[leg] = (line.get(leg) or {}).get("rank_check")
+    for leg, v in (line.get("small") or {}).items():
+        if isinstance(v, dict):
+            rc["small_" + leg] = v.get("rank_check")
+    rc = {k: bool(v.get("bit_exact")) for k, v in rc.items() if isinstance(v, dict)}
+    if rc:
+        h["rank_check_bit_exact"] = rc
     if detail_path:
         h["detail"] = detail_path
     # never let the line outgrow the driver's capture: drop the least important parts first
@@ -648,6 +660,36 @@ def shard_proxy(args, full_ms: float, full_value: float, unit: str, time_rank):
     return out
 
 
+def rank_check(args, D, rank, world, what: str, local: int, units: int, full_pass):
+    """world > 1, strong scaling: every rank's shard outputs against a 1-rank pass of the whole set.
+    Each rank sends one (digest, units) pair (shard.digest: the units hashed with their global keys);
+    rank 0 then runs the whole set by itself on its GPU (full_pass(world) -> (digest of everything,
+    [digest of rank r's range for r in 0..world-1], units)) and compares: the gathered digests sum to the
+    1-rank pass's and each rank's equals the 1-rank pass's over the same range. A mismatch fails the run
+    on rank 0. The other ranks go on to the next leg's barrier meanwhile. Returns the check (rank 0)."""
+    if world == 1 or args.scaling != "strong" or args.no_rank_check:
+        return None
+    from genomicsbench_palisade_amd import shard
+    import torch.distributed as dist
+    got = [None] * world
+    dist.all_gather_object(got, (int(local), int(units)))
+    if rank != 0:
+        return None
+    log(f"{what}: 1-rank pass of the whole set on rank 0 (gathered-output check)")
+    t0 = time.perf_counter()
+    full, per, nfull = full_pass(world)
+    gathered = shard.digest_add(*[g[0] for g in got])
+    match = [int(g[0]) == int(p) for g, p in zip(got, per)]
+    out = {"world": world, "units": int(sum(g[1] for g in got)), "units_1rank": int(nfull),
+           "bit_exact": bool(gathered == full and all(match) and sum(g[1] for g in got) == nfull),
+           "per_rank_match": match, "digest": f"{full:016x}", "check_s": round(time.perf_counter() - t0, 2),
+           "against": "a 1-rank pass of the whole set on rank 0's GPU; units hashed with their global keys "
+                      "(shard.digest), gathered one digest per rank"}
+    if not out["bit_exact"]:
+        raise SystemExit(f"{what}: gathered {world}-rank outputs differ from the 1-rank pass: {out}")
+    return out
+
+
 def e2e_time(fn, reps: int = 2) -> float:
     """Mean wall seconds of fn() over `reps` calls after one warm call (host arrays in, host arrays out)."""
     fn()
@@ -782,6 +824,32 @@ def bench_chain(args, D, rank, world, kind="large"):
                      "unit": "T int32/fp64 op/s", "frac": ach / PEAK_CHAIN_OPS, "ops_per_visited_pair": CHAIN_OPS_PER_PAIR},
         "kernels_ms": {"chain_dp (all kernels of a step)": ms},
     }
+    # the speculative segments' bookkeeping (chain_split.hip): a failed guess costs a sequential
+    # fix-up and a re-mark of its call, so a nonzero count is worth seeing beside the time
+    nsplit, rounds, fixups = b.split_stats()
+    out["split_stats"] = {"split_calls": nsplit, "verify_rounds": rounds, "fixup_blocks": fixups}
+    if fixups:
+        log(f"chain {kind}: WARNING {fixups} speculative-segment fix-ups in the last step (window cap / warm-up "
+            f"too short for these calls)")
+    if world > 1:
+        a0 = int(full.offsets[lo])
+        r4 = b.results()[:4]
+        keys = a0 + np.arange(len(r4[0]), dtype=np.int64)
+
+        def full_pass(w):
+            fb = chain.ChainBatch(full)
+            fb.run()
+            f4 = fb.results()[:4]
+            fb.close()
+            fk = np.arange(len(f4[0]), dtype=np.int64)
+            per = []
+            for r in range(w):
+                c0, c1 = shard.call_range(full, r, w)
+                s = slice(int(full.offsets[c0]), int(full.offsets[c1]))
+                per.append(shard.digest(fk[s], *[x[s] for x in f4]))
+            return shard.digest(fk, *f4), per, len(fk)
+        out["rank_check"] = rank_check(args, D, rank, world, f"chain {kind}", shard.digest(keys, *r4), len(keys),
+                                       full_pass)
     if proxy_on(args, world):
         log(f"chain {kind}: shard proxy of {args.shard_of}")
 
@@ -959,6 +1027,23 @@ def bench_bsw(args, D, rank, world, kind="large"):
                      "frac": ach / PEAK_INT_OPS, "ops_per_cell": BSW_OPS_PER_CELL},
         "kernels_ms": {"bsw (all launches of a step)": ms},
     }
+    if world > 1:
+        keys = lo + np.arange(pairs.n, dtype=np.int64)
+        o6 = out6[:pairs.n]
+
+        def full_pass(w):
+            fb = bsw.BswBatch(full, params)
+            fb.run()
+            f6 = fb.results(want_cells=False)[0][:full.n]
+            fb.close()
+            fk = np.arange(full.n, dtype=np.int64)
+            per = []
+            for r in range(w):
+                p0, p1 = shard.pair_range(full, r, w)
+                per.append(shard.digest(fk[p0:p1], *f6[p0:p1].T))
+            return shard.digest(fk, *f6.T), per, full.n
+        out["rank_check"] = rank_check(args, D, rank, world, f"bsw {kind}", shard.digest(keys, *o6.T), pairs.n,
+                                       full_pass)
     if proxy_on(args, world):
         log(f"bsw {kind}: shard proxy of {args.shard_of}")
 
@@ -1078,6 +1163,20 @@ def bench_phmm(args, D, rank, world, kind="large"):
         "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
     }
+    if world > 1:
+        def full_pass(w):
+            fj = phmm.DeviceBatch(full)
+            fj.run()
+            fres, _, _, fused, _ = fj.results()
+            fj.close()
+            fk = np.arange(full.n, dtype=np.int64)
+            per = []
+            for r in range(w):
+                ix = shard.testcase_index(full, r, w)
+                per.append(shard.digest(ix, fres[ix], fused[ix]))
+            return shard.digest(fk, fres[:full.n], fused[:full.n]), per, full.n
+        out["rank_check"] = rank_check(args, D, rank, world, f"phmm {kind}",
+                                       shard.digest(tidx, res[:ta.n], used[:ta.n]), ta.n, full_pass)
     if proxy_on(args, world):
         log(f"phmm {kind}: shard proxy of {args.shard_of}")
 
@@ -1148,6 +1247,7 @@ def bench_fmi(args, D, rank, world):
         a, _, calls[0] = rs.timing()
         return a
     elapsed, ms = timed_steps(D, args.steps, step)
+    rcheck = fmi_rank_check(args, D, rank, world, "fmi large", fmi, shard, idx, rs, codes_all, lens_all, lo)
     calls = calls[0]
     reads_all = D.sum(float(len(lens)))
     mreads = reads_all * args.steps / elapsed / 1e6
@@ -1206,6 +1306,7 @@ def bench_fmi(args, D, rank, world):
         "dropin_e2e": e2e,
         "sa_lookup": sa,
         "shard_proxy": proxy,
+        "rank_check": rcheck,
         "small": small,
     }
 
@@ -1296,6 +1397,37 @@ def bench_fmi_human(args, D, rank, world):
         "parity_check": check,
         "cpu_baseline": cpu,
     }
+
+
+def _smem_digest(shard, sm, bc, first_batch, rid0=0):
+    """rid0: the shard's first read (a shard's search numbers its reads from 0)."""
+    keys = shard.smem_keys(sm["rid"], bc, first_batch)
+    rid = sm["rid"].astype(np.int64) + rid0
+    return shard.digest(keys, rid, *[sm[f] for f in ("m", "n", "k", "l", "s")])
+
+
+def fmi_rank_check(args, D, rank, world, what, fmi, shard, idx, rs, codes_all, lens_all, lo):
+    """rank_check for an fmi set: the rank's SMEMs (in fmi.cpp's per-batch order) keyed by (global
+    batch, position in batch), against a 1-rank search of every read on rank 0."""
+    if world == 1 or args.scaling != "strong" or args.no_rank_check:
+        return None
+    sm, tot, bc, _ = rs.results(batch_size=shard.FMI_BATCH)
+    local = _smem_digest(shard, sm, bc, lo // shard.FMI_BATCH, lo)
+    del sm
+
+    def full_pass(w):
+        fr = fmi.Reads(idx, codes_all, lens_all)
+        fr.search(19)
+        fsm, ftot, fbc, _ = fr.results(batch_size=shard.FMI_BATCH)
+        fr.close()
+        starts = np.concatenate([[0], np.cumsum(fbc)])
+        per = []
+        for r in range(w):
+            r0, r1 = shard.read_range(len(lens_all), r, w)
+            b0, b1 = r0 // shard.FMI_BATCH, (r1 + shard.FMI_BATCH - 1) // shard.FMI_BATCH
+            per.append(_smem_digest(shard, fsm[starts[b0]:starts[b1]], fbc[b0:b1], b0))
+        return _smem_digest(shard, fsm, fbc, 0), per, ftot
+    return rank_check(args, D, rank, world, what, local, tot, full_pass)
 
 
 def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full_value):
@@ -1390,13 +1522,14 @@ def bench_fmi_small(args, D, rank, world, fmi, gen, shard, idx, ref):
         return a
     elapsed, ms = timed_steps(D, args.steps, step)
     _, total, _, _ = rs.results(batch_size=512, want_smems=False)
+    rcheck = fmi_rank_check(args, D, rank, world, "fmi small", fmi, shard, idx, rs, codes_all, lens_all, lo)
     rs.close()
     nr = hi - lo
     alg = calls[0] * FMI_BYTES_PER_EXT + nr * 151 + total * 40
     value = D.sum(float(nr)) * args.steps / elapsed / 1e6
     proxy = fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, elapsed / args.steps * 1e3, value) \
         if proxy_on(args, world) else None
-    return {"value": round(value, 3), "unit": "Mreads/s", "shard_proxy": proxy,
+    return {"value": round(value, 3), "unit": "Mreads/s", "shard_proxy": proxy, "rank_check": rcheck,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "config": {"workload": f"fmi small: {len(lens_all)} reads x 151 bp over the large index; "
                                    + shard_note(args, "reads", lo, hi, len(lens_all), world),
@@ -1471,9 +1604,85 @@ def cpu_baseline_sa(oi, codes, lens, sample_seconds: float):
                       f"(max_occ 500), {reps} pass(es) over {threads} threads, {t:.1f} s"}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def child_envs(n: int, port: int, base=None):
+    """The environments of the N ranks `bench.py --gpus N` starts when no launcher set WORLD_SIZE: one
+    process per GPU, ranks 0..N-1 (LOCAL_RANK = RANK: one node), rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append(e)
+    return out
+
+
+def launch(n: int, argv, dry_run: bool = False, cmd=None, poll_s: float = 0.5) -> int:
+    """`bench.py --gpus N` with WORLD_SIZE unset: start N fresh rank processes of this script (the
+    same arguments, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, as torch.distributed.run would) and
+    wait for them. This parent never imports torch or the package, so it never touches the GPU (the
+    box forbids exec'ing after GPU initialisation; the ranks are children, not execs). Rank 0's stdout
+    (the one JSON line) is this process's stdout; the other ranks' stdout goes to stderr. When a rank
+    fails, the others are terminated and the first failing status is returned."""
+    import subprocess
+    port = _free_port()
+    cmd = list(cmd) if cmd is not None else [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    envs = child_envs(n, port)
+    keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+    if dry_run:
+        for e in envs:
+            print(json.dumps({"cmd": cmd, "env": {k: e[k] for k in keys}}), flush=True)
+        return 0
+    log(f"launching {n} ranks on 127.0.0.1:{port}: {' '.join(cmd)}")
+    sys.stdout.flush()
+    procs = [subprocess.Popen(cmd, env=e, stdout=None if r == 0 else sys.stderr, start_new_session=False)
+             for r, e in enumerate(envs)]
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad and status == 0:
+                status = bad[0]
+                log(f"a rank exited with status {status}; terminating the others")
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+            if all(c is not None for c in codes):
+                break
+            time.sleep(poll_s)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise
+    finally:
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return status if status >= 0 else 128 - status
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (= ranks) of the run; without a launcher's WORLD_SIZE, bench.py starts the N rank "
+                         "processes itself (one per GPU)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the N rank processes' command and environment that --gpus N would start, then exit")
+    ap.add_argument("--no-rank-check", action="store_true",
+                    help="world > 1: skip the gathered-output check against a 1-rank pass on rank 0")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
@@ -1503,6 +1712,17 @@ def main():
                     help="where the full record goes (shard proxies, drop-ins, traffic detail, parity checks); "
                          "stdout carries only the compact headline line ('' = no file)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} (from the launcher) does not match "
+                  f"--gpus {args.gpus}", file=sys.stderr)
+            raise SystemExit(2)
+        if args.launch_dry_run:
+            raise SystemExit("--launch-dry-run is for the self-launching form (WORLD_SIZE unset)")
+    elif args.gpus > 1 or args.launch_dry_run:
+        raise SystemExit(launch(args.gpus, sys.argv[1:], dry_run=args.launch_dry_run))
 
     world, rank, local = dist_env()
     D = Dist(world)
@@ -1560,6 +1780,7 @@ def main():
             "roofline_f64": ph["roofline_f64"] if ph else None,
             "kernels_ms": ph["kernels_ms"] if ph else None,
             "shard_proxy": ph.get("shard_proxy") if ph else None,
+            "rank_check": ph.get("rank_check") if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
             "dropin_e2e": ph.get("dropin_e2e") if ph else None,
             "fmi": fm,

@@ -446,7 +446,10 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   // Tiles of at most ~256 MB of `prev` scratch ((maxlen + 1) entries per task): the per-thread
   // workspace stays bounded whatever the batch. Per tile: the whole tile, then its overflowing
   // subset with a slot sized to its largest count.
-  int64_t tile = std::max<int64_t>(64, ((256ll << 20) / ((int64_t)(maxlen + 2) * (int64_t)sizeof(TEnt))) & ~63ll);
+  // (getSMEMs takes reads of any length: for ~Mb reads the tile falls below a wave's 64 tasks rather
+  // than the scratch growing past the bound)
+  int64_t tile = std::max<int64_t>(1, (256ll << 20) / ((int64_t)(maxlen + 2) * (int64_t)sizeof(TEnt)));
+  if (tile >= 64) tile &= ~63ll;
   if (const char *te = getenv("GB_FMI_TASK_TILE")) tile = std::max(1, atoi(te));  // tests: force many tiles
   bool uploaded = false;
   int64_t calls_sum = 0;

@@ -496,6 +496,247 @@ __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__rest
   return na;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two rows per lane (the f32 pass over LDS stacks). A stripe is 128 rows: lane k owns rows 2k (a)
+// and 2k+1 (b), and row rho of the stripe is at column t - rho + 1 at step t, as before. Row b runs
+// one column behind row a in the same lane, so its inputs from the row above (X = w and the bracket
+// z of row a) are row a's previous-step values, carried in registers; only row a's inputs cross a
+// lane (lane k-1's row b, DPP wave_shr). Per two cells: 24 FP ops, 2 DPP moves, 2 selects, one LDS
+// code read (row b reuses row a's code of the step before) -- against 2 DPP moves and 2 code reads
+// per two cells with one row per lane. The arithmetic of each cell is unchanged (same operands,
+// same order), so the results are bit-identical.
+constexpr int kRows2 = 2 * kWave;  // stripe height
+constexpr int kBndPad2 = 136;      // records / codes beyond column C (lane 0 reads up to C + kRows2 + 2)
+constexpr int kCodePad2 = kRows2;  // codes below column 0 (lane 63's row a starts at column -125)
+constexpr int kNoWrite2 = kRows2 - 4;  // lane 63's row b writes from column -2 on (step 124)
+
+// One row's constants and initial state (phmm_stack's per-lane set-up, for stripe row rho): r is the
+// row's place in its testcase (0: va, 1: v0, 2..R+1: read row r-2); z_top the bracket lane 0's first
+// row takes from the record at column 0.
+template <typename T>
+__device__ __forceinline__ void setup_row(int rho, bool dead, int r, int R, const uint8_t *__restrict__ rbase,
+                                          const DevTab<T> &tab, T init_Y, T z_top, RowParams<T> &P,
+                                          LaneState<T> &st) {
+  st.Mp = st.zo = st.wo = (T)0;
+  st.Yp = (T)0;
+  st.zd = rho == 0 ? z_top : (T)0;
+  T pMM, pGAPM, pMX, pXX, a, b, dm, dx;
+  uint32_t f;
+  const T zero = (T)0, one = (T)1;
+  P.nMM = P.nGAPM = P.nGAPMx = P.nMX = P.nXX = zero;
+  if (dead) {
+    P.pMY = P.pYY = P.dmatch = P.dmis = zero;
+    P.rmask = 0;
+  } else if (r == 0) {  // va
+    P.pMY = zero;
+    P.pYY = one;
+    P.dmatch = P.dmis = zero;
+    P.rmask = 0;
+    P.nGAPM = one;
+    st.Yp = init_Y;
+    st.zo = (zero * zero + zero * zero) + init_Y * one;
+  } else if (r == 1) {  // v0
+    P.pMY = P.pYY = zero;
+    P.dmatch = one;
+    P.dmis = zero;
+    P.rmask = 0x3F;
+    load_row(rbase, R, 0, tab, pMM, pGAPM, pMX, pXX, a, b, dm, dx, f);
+    P.nMM = pGAPM;
+    st.zd = init_Y;
+    if (rho == 0) st.zo = (init_Y * P.nMM + zero * zero) + zero * zero;
+  } else {
+    load_row(rbase, R, r - 2, tab, pMM, pGAPM, pMX, pXX, P.pMY, P.pYY, P.dmatch, P.dmis, P.rmask);
+    if (r - 1 < R) {
+      load_row(rbase, R, r - 1, tab, P.nMM, P.nGAPM, P.nMX, P.nXX, a, b, dm, dx, f);
+      P.nGAPMx = P.nGAPM;
+    }
+  }
+}
+
+// One step of both rows: row b (column c - 1) from row a's previous-step partials, row a (column c)
+// from lane k-1's row b (previous step) or, in lane 0, the record of the stripe above.
+template <typename T, bool kSum, bool kWrite>
+__device__ __forceinline__ void phmm_step2(const Brec<T> &rec, uint32_t h, uint32_t &hb, LaneState<T> &A,
+                                           LaneState<T> &B, const RowParams<T> &PA, const RowParams<T> &PB,
+                                           T &sMa, T &sXa, T &sMb, T &sXb, Brec<T> *wr, bool last_lane) {
+  const T Xb = A.wo;
+  const T zdnb = A.zo;
+  const T Xa = dpp<dpp_shr>(B.wo, rec.w);
+  const T zdna = dpp<dpp_shr>(B.zo, rec.z);
+  const T Mb = B.zd * select_dist(PB.rmask, hb, PB.dmatch, PB.dmis);
+  const T Ma = A.zd * select_dist(PA.rmask, h, PA.dmatch, PA.dmis);
+  const T Yb = B.Mp * PB.pMY + B.Yp * PB.pYY;
+  const T Ya = A.Mp * PA.pMY + A.Yp * PA.pYY;
+  B.zo = (Mb * PB.nMM + Xb * PB.nGAPMx) + Yb * PB.nGAPM;
+  B.wo = Mb * PB.nMX + Xb * PB.nXX;
+  A.zo = (Ma * PA.nMM + Xa * PA.nGAPMx) + Ya * PA.nGAPM;
+  A.wo = Ma * PA.nMX + Xa * PA.nXX;
+  if constexpr (kSum) {
+    sMa = sMa + Ma;
+    sXa = sXa + Xa;
+    sMb = sMb + Mb;
+    sXb = sXb + Xb;
+  }
+  if constexpr (kWrite) {
+    if (last_lane) {
+      Brec<T> r;
+      r.z = B.zo;
+      r.w = B.wo;
+      *wr = r;
+    }
+  }
+  A.zd = zdna;
+  A.Mp = Ma;
+  A.Yp = Ya;
+  B.zd = zdnb;
+  B.Mp = Mb;
+  B.Yp = Yb;
+  hb = h;
+}
+
+// Sweep `steps` anti-diagonals of a 128-row stripe, 4 per iteration. Last rows: row rho of the stripe
+// reaches column C at step C + rho - 1, where its sum is final (pa: rows a by lane, pb: rows b).
+template <typename T, bool kSum, bool kWrite>
+__device__ __forceinline__ void phmm_stripe2(int steps, LaneState<T> &A, LaneState<T> &B, const RowParams<T> &PA,
+                                             const RowParams<T> &PB, Brec<T> *__restrict__ bnd,
+                                             const uint8_t *__restrict__ hcol, int C, int lane, uint64_t pa,
+                                             uint64_t pb, T *__restrict__ outA, T *__restrict__ outB) {
+  const uint8_t *hl = hcol + 1 - 2 * lane;
+  const bool last_lane = lane == kWave - 1;
+  constexpr int U = 4;
+  T sMa = (T)0, sXa = (T)0, sMb = (T)0, sXb = (T)0;
+  uint32_t hb = hl[-1];  // row b's code at its column before step 0
+  auto next_target = [&]() -> int {
+    if (!kSum || !(pa | pb)) return INT_MAX;
+    const int ra = pa ? 2 * __builtin_ctzll(pa) : INT_MAX / 2;
+    const int rb = pb ? 2 * __builtin_ctzll(pb) + 1 : INT_MAX / 2;
+    return C + min(ra, rb) - 1;
+  };
+  int target = next_target();
+  auto single = [&](int tt, auto wr_tag) {
+    constexpr bool W = decltype(wr_tag)::value;
+    phmm_step2<T, kSum, W>(bnd[tt + 1], hl[tt], hb, A, B, PA, PB, sMa, sXa, sMb, sXb, bnd + (tt - (kRows2 - 2)),
+                           last_lane);
+    if (kSum && tt == target) {
+      const int rho = tt - C + 1;
+      if (rho & 1) {
+        if (lane == (rho >> 1)) *outB = sMb + sXb;
+        pb &= pb - 1;
+      } else {
+        if (lane == (rho >> 1)) *outA = sMa + sXa;
+        pa &= pa - 1;
+      }
+      target = next_target();
+    }
+  };
+  int vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  Brec<T> *wb = bnd - (kRows2 - 2) + vzero;
+  auto run = [&](int t, int end, auto wr_tag) {
+    constexpr bool W = decltype(wr_tag)::value;
+    for (; t + U <= end; t += U) {
+      if (kSum && target < t + U) {
+        for (int u = 0; u < U; u++) single(t + u, wr_tag);
+        continue;
+      }
+      Brec<T> *wr = wb + t;
+      const Brec<T> c0 = wr[kRows2 - 1], c1 = wr[kRows2], c2 = wr[kRows2 + 1], c3 = wr[kRows2 + 2];
+      const uint32_t h0 = hl[t], h1 = hl[t + 1], h2 = hl[t + 2], h3 = hl[t + 3];
+      phmm_step2<T, kSum, W>(c0, h0, hb, A, B, PA, PB, sMa, sXa, sMb, sXb, wr, last_lane);
+      phmm_step2<T, kSum, W>(c1, h1, hb, A, B, PA, PB, sMa, sXa, sMb, sXb, wr + 1, last_lane);
+      phmm_step2<T, kSum, W>(c2, h2, hb, A, B, PA, PB, sMa, sXa, sMb, sXb, wr + 2, last_lane);
+      phmm_step2<T, kSum, W>(c3, h3, hb, A, B, PA, PB, sMa, sXa, sMb, sXb, wr + 3, last_lane);
+    }
+    for (; t < end; t++) single(t, wr_tag);
+  };
+  if constexpr (kWrite) {
+    const int a = min(steps, kNoWrite2);
+    run(0, a, std::false_type{});
+    run(a, steps, std::true_type{});
+  } else {
+    run(0, steps, std::false_type{});
+  }
+}
+
+// phmm_stack with two rows per lane (f32 pass, every testcase of the stack).
+template <typename T>
+__device__ __forceinline__ void phmm_stack2(const Stack &S, const uint32_t *__restrict__ stk_tc,
+                                            const TcDesc *__restrict__ descs, const uint8_t *__restrict__ pool,
+                                            const DevTab<T> &tab, T *__restrict__ raw_out, uint8_t *smem_raw) {
+  const int lane = threadIdx.x;
+  const int C = (int)S.C;
+  Brec<T> *bnd = reinterpret_cast<Brec<T> *>(smem_raw) + kRecPad;
+  uint8_t *hcol = smem_raw + sizeof(Brec<T>) * (size_t)(C + kBndPad2 + kRecPad) + kCodePad2;
+  const int na = (int)S.count;
+  TcDesc d = {0, 0, 0, 0};
+  if (lane < na) d = descs[stk_tc[S.first + lane]];
+  const int rows = lane < na ? (int)(d.dims & 0xffff) + 2 : 0;
+  const int incl = scan_add(rows);
+  const int T_rows = __builtin_amdgcn_readlane(incl, 63);
+  const int e_start = incl - rows, e_R = rows - 2;  // entry a in lane a
+  const T init_Y = tab.init_const / (T)C;
+  const uint8_t *hcode = pool + S.hap_off;
+  for (int c = lane; c < C + kBndPad2; c += kWave) {
+    Brec<T> b;
+    b.z = (T)0;
+    b.w = (T)0;
+    bnd[c] = b;
+  }
+  for (int c = lane - kCodePad2; c < C + kBndPad2; c += kWave)
+    hcol[c] = (c >= 1 && c <= C) ? hcode[c - 1] : (c == 0 ? 5 : (c < 0 ? 6 : 0));
+  __syncthreads();
+
+  const int nstripes = (T_rows + kRows2 - 1) / kRows2;
+  for (int s = 0; s < nstripes; s++) {
+    const int g0 = s * kRows2 + 2 * lane, g1 = g0 + 1;
+    int lo = 0, hi = na - 1;
+    while (__builtin_amdgcn_ballot_w64(lo < hi)) {
+      const int mid = (lo + hi + 1) >> 1;
+      const int sm = __shfl(e_start, mid);
+      if (lo < hi) {
+        if (sm <= g0) lo = mid; else hi = mid - 1;
+      }
+    }
+    // row b: the same testcase, or the next one when it starts at g1
+    const int nxt = __shfl(e_start, min(lo + 1, kWave - 1));
+    const int lob = (lo + 1 < na && nxt <= g1) ? lo + 1 : lo;
+    const int sa = __shfl(e_start, lo), Ra = __shfl(e_R, lo);
+    const uint32_t rda = (uint32_t)__shfl((int)d.read_off, lo), oa = (uint32_t)__shfl((int)d.out_idx, lo);
+    const int sb = __shfl(e_start, lob), Rb = __shfl(e_R, lob);
+    const uint32_t rdb = (uint32_t)__shfl((int)d.read_off, lob), ob = (uint32_t)__shfl((int)d.out_idx, lob);
+    const int ra = g0 - sa, rb = g1 - sb;
+    const bool deadA = g0 >= T_rows, deadB = g1 >= T_rows;
+    RowParams<T> PA, PB;
+    LaneState<T> A, B;
+    const T z_top = lane == 0 ? bnd[0].z : (T)0;
+    setup_row<T>(2 * lane, deadA, ra, Ra, pool + rda, tab, init_Y, z_top, PA, A);
+    setup_row<T>(2 * lane + 1, deadB, rb, Rb, pool + rdb, tab, init_Y, (T)0, PB, B);
+    const uint64_t pa = __builtin_amdgcn_ballot_w64(!deadA && ra == Ra + 1);
+    const uint64_t pb = __builtin_amdgcn_ballot_w64(!deadB && rb == Rb + 1);
+    const bool more = s < nstripes - 1;
+    const int steps = more ? C + kRows2 - 1 : C + (T_rows - s * kRows2) - 1;
+    T *outA = raw_out + oa, *outB = raw_out + ob;
+    if (pa | pb) {
+      if (more)
+        phmm_stripe2<T, true, true>(steps, A, B, PA, PB, bnd, hcol, C, lane, pa, pb, outA, outB);
+      else
+        phmm_stripe2<T, true, false>(steps, A, B, PA, PB, bnd, hcol, C, lane, pa, pb, outA, outB);
+    } else {
+      phmm_stripe2<T, false, true>(steps, A, B, PA, PB, bnd, hcol, C, lane, 0, 0, outA, outB);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void phmm_forward2(const Stack *__restrict__ stacks,
+                                                     const uint32_t *__restrict__ stk_tc,
+                                                     const TcDesc *__restrict__ descs,
+                                                     const uint8_t *__restrict__ pool, DevTab<float> tab,
+                                                     float *__restrict__ raw_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  phmm_stack2<float>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, smem_raw);
+}
+
 // f32 pass: one stack per workgroup (LPT order). f64 pass: a persistent grid takes stacks through
 // counter[1] and recomputes their testcases whose f32 result fell below MIN_ACCEPTED; counter[0]
 // counts them.
@@ -598,7 +839,8 @@ int get_device_tables(DeviceTables **out) {
   if (st) return st;
   st = upload_tables(*g_hd, &t->d);
   if (st) return st;
-  for (auto fn : {(const void *)phmm_forward<float, false>, (const void *)phmm_forward<double, true>})
+  for (auto fn : {(const void *)phmm_forward<float, false>, (const void *)phmm_forward<double, true>,
+                  (const void *)phmm_forward2})
     GB_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   g_dev[dev] = t;
   *out = t;
@@ -669,6 +911,7 @@ struct gb_phmm_batch {
   int cus = 256;                   // compute units of the device (stack height rule)
   bool ran = false;
   bool force_f64 = false;
+  int rpl = 2;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=1: one, for A/B probes)
 };
 
 extern "C" {
@@ -869,6 +1112,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   // 256 4.64 per step; on the whole job 2048 rows stay best (33.0 ms; 512: 33.7).
   int64_t total_rows = 0;
   for (int k = 0; k < n; k++) total_rows += (int64_t)(desc[k].dims & 0xffff) + 2;
+  b->rpl = 2;
+  if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 1 ? 1 : 2;  // probes: one row per lane
   int stack_rows = kStackRows;
   while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
@@ -884,7 +1129,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       k++;
     }
     stacks.push_back(S);
-    scost.push_back((uint64_t)((rows + kWave - 1) / kWave) * (uint64_t)(C + kWave));
+    const int sh = b->rpl == 2 ? kRows2 : kWave;  // stripe height of the f32 pass
+    scost.push_back((uint64_t)((rows + sh - 1) / sh) * (uint64_t)(C + sh));
   }
   // by decreasing cost (stable), the stacks whose haplotype does not fit the LDS behind the others
   // (they run on the kLong kernels)
@@ -1047,10 +1293,16 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
     const int ns = b->nstacks, nl = b->n_long;
     const Stack *d_long = b->d_stacks + ns;
     if (!b->force_f64) {
-      if (ns > 0)
+      if (ns > 0 && b->rpl == 2) {
+        const size_t lds_f2 = sizeof(Brec<float>) * (size_t)(b->max_haplen + kBndPad2 + kRecPad) +
+                              (size_t)(b->max_haplen + kBndPad2 + kCodePad2) + 16;
+        hipLaunchKernelGGL(phmm_forward2, dim3(ns), dim3(kWave), lds_f2, b->stream, b->d_stacks, b->d_stk_tc,
+                           b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf);
+      } else if (ns > 0) {
         hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
                            b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
                            b->d_count, 0, (uint8_t *)nullptr, (size_t)0);
+      }
       if (nl > 0)
         hipLaunchKernelGGL((phmm_forward<float, false, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
                            nl, b->d_stk_tc, b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,

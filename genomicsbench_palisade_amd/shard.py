@@ -101,3 +101,65 @@ def pair_range(pairs, rank: int, world: int):
 def shard_pairs(pairs, rank: int, world: int):
     lo, hi = pair_range(pairs, rank, world)
     return pairs.slice(lo, hi), (lo, hi)
+
+
+# ---- output digests: a rank's shard outputs against a 1-rank pass, without moving the outputs ------
+# Each output unit (a testcase's result, an anchor's chain_dp outputs, an SMEM at its place in its
+# batch, a pair's six fields) hashes together with its GLOBAL key (testcase index, anchor index,
+# (batch, position in batch), pair index); a set's digest is the sum of its units' hashes mod 2^64. The
+# sum does not depend on how the units are split over ranks, and the keys make it order-sensitive, so
+# sum(rank digests) == digest(1-rank pass) iff every unit landed where the 1-rank pass puts it (up to a
+# 2^-64 collision). bench.py gathers one (digest, units) pair per leg and rank.
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def mix64(x):
+    """splitmix64's finaliser over a uint64 array (wrapping arithmetic)."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * _M1
+        x = (x ^ (x >> np.uint64(27))) * _M2
+        return x ^ (x >> np.uint64(31))
+
+
+def _as_u64(c):
+    c = np.asarray(c)
+    if c.dtype.kind == "f":
+        c = c.view(np.uint64 if c.itemsize == 8 else np.uint32)
+    return c.astype(np.int64).view(np.uint64) if c.dtype.kind == "i" else c.astype(np.uint64)
+
+
+def unit_hashes(keys, *cols):
+    """Per-unit 64-bit hashes of (key, col0[i], col1[i], ...); floats hash by their bits."""
+    with np.errstate(over="ignore"):
+        h = (_as_u64(keys) ^ _GOLD) * _M1
+        for c in cols:  # xor-multiply-shift per column (4 array ops), one full finaliser at the end
+            h ^= _as_u64(c)
+            h *= _M2
+            h ^= h >> np.uint64(29)
+        return mix64(h)
+
+
+def digest(keys, *cols) -> int:
+    """sum(unit_hashes) mod 2^64 as a Python int (0 for no units)."""
+    if len(keys) == 0:
+        return 0
+    return int(np.add.reduce(unit_hashes(keys, *cols), dtype=np.uint64))
+
+
+def digest_add(*ds) -> int:
+    return sum(int(d) for d in ds) % (1 << 64)
+
+
+def smem_keys(rid, batch_counts, first_batch: int):
+    """fmi: the global key of each SMEM of a shard's output -- (global batch, position inside the batch)
+    -- from the per-batch counts of the shard (its batches are whole, the first one `first_batch`)."""
+    bc = np.asarray(batch_counts, np.int64)
+    starts = np.repeat(np.cumsum(bc) - bc, bc)
+    pos = np.arange(len(starts), dtype=np.int64) - starts
+    b = np.repeat(np.arange(first_batch, first_batch + len(bc), dtype=np.int64), bc)
+    if len(rid) != len(pos):
+        raise ValueError("SMEM count does not match the per-batch counts")
+    return (b << 32) | pos

@@ -49,12 +49,38 @@ rlo, rhi = shard.read_range(len(lens), rank, world)
 oi = fmi_util.OracleIndex(ref)
 fs, fbc, _ = oi.run(codes[rlo:rhi], lens[rlo:rhi], batch_size=512)
 fs["rid"] += rlo
+# bench.rank_check: one digest per rank gathered, rank 0 compares with a 1-rank pass (here the oracle
+# over the whole set stands in for the GPU pass); a corrupted shard must fail the check
+a0 = int(calls.offsets[lo])
+r4 = oracle_lib.chain_oracle(sub, 1)[:4] if sub.ncalls else [np.zeros(0, np.int32)] * 4
+keys = a0 + np.arange(sub.nanchors, dtype=np.int64)
+def full_pass(w):
+    f4 = [x[:calls.nanchors] for x in oracle_lib.chain_oracle(calls, 1)[:4]]
+    fk = np.arange(calls.nanchors, dtype=np.int64)
+    per = []
+    for r in range(w):
+        c0, c1 = shard.call_range(calls, r, w)
+        s = slice(int(calls.offsets[c0]), int(calls.offsets[c1]))
+        per.append(shard.digest(fk[s], *[x[s] for x in f4]))
+    return shard.digest(fk, *f4), per, len(fk)
+rargs = types.SimpleNamespace(scaling="strong", no_rank_check=False)
+rc = bench.rank_check(rargs, D, rank, world, "chain test", shard.digest(keys, *[x[:sub.nanchors] for x in r4]),
+                      sub.nanchors, full_pass)
+bad = [x[:sub.nanchors].copy() for x in r4]
+if rank == 1 and sub.nanchors:
+    bad[0][sub.nanchors // 2] += 1
+try:
+    bench.rank_check(rargs, D, rank, world, "chain test", shard.digest(keys, *bad), sub.nanchors, full_pass)
+    caught = False
+except SystemExit:
+    caught = True
 import torch.distributed as dist
 got = [None] * world
 dist.all_gather_object(got, {"chain": sc.tolist(), "bsw": out.tolist(), "phmm": pr.tolist(), "tidx": [int(x) for x in tidx],
                              "fmi": [list(map(int, t)) for t in zip(fs["rid"], fs["m"], fs["n"], fs["k"], fs["l"], fs["s"])],
                              "fmi_bc": fbc.tolist(), "rrange": [rlo, rhi],
-                             "max": mx, "sum": sm, "range": [lo, hi], "timed_steps_ms": ms})
+                             "max": mx, "sum": sm, "range": [lo, hi], "timed_steps_ms": ms,
+                             "rank_check": rc, "caught": caught})
 if rank == 0:
     json.dump(got, open(os.environ["GB_OUT"], "w"))
 D.close()
@@ -113,6 +139,11 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
     fb = oracle_lib.bsw_oracle(pairs, bsw.default_params(), 1)[0]
     assert (np.array(got[0]["bsw"] + got[1]["bsw"], np.int32).reshape(-1, 6) == fb).all()
     assert [g["timed_steps_ms"] for g in got] == [1.5, 1.5]
+    # bench.rank_check: rank 0 holds the check; the corrupted rank-1 shard was caught on rank 0 only
+    rc = got[0]["rank_check"]
+    assert rc["bit_exact"] and rc["per_rank_match"] == [True, True] and rc["units"] == calls.nanchors
+    assert got[1]["rank_check"] is None
+    assert [g["caught"] for g in got] == [True, False]
     # phmm: testcase shards balanced by cells concatenate to the 1-rank results
     import ctypes
     from genomicsbench_palisade_amd._tc import TestcaseArray

@@ -1,0 +1,106 @@
+"""Stale-LDS guard (GPU): every CU's LDS is first filled with an adversarial pattern
+(tests/cpp/lds_poison.hip: all ones, word index + 1, small constants that equal an "i + 1" stamp of
+an early anchor, hashed words), then the LDS-heavy kernels run on inputs whose outputs depend on their
+LDS words -- chain_rows + verify_lanes (stamp rings, the split path), smem_search (the LDS `prev` head
+and staged read codes), bsw_lane_kernel (query codes) -- and must stay oracle-exact. A kernel that reads
+a word it did not write in its own workgroup (chain_rows' stamps before commit 1da81ef) fails here
+deterministically instead of once in a while."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import fmi_util
+import oracle_lib
+from conftest import ROOT
+from genomicsbench_palisade_amd import gen
+
+pytestmark = pytest.mark.gpu
+
+# (mode, value): 0 all ones, 1 word + 1, 2 constant, 3 word + constant, 4 hashed
+PATTERNS = [(0, 0), (1, 0), (2, 2), (2, 37), (2, 300), (3, 1000), (4, 0)]
+
+
+@pytest.fixture(scope="module")
+def poison():
+    path = os.path.join(ROOT, "tests", "_build", "liblds_poison.so")
+    if not os.path.exists(path):
+        pytest.fail(f"{path} not built (make)")
+    lib = ctypes.CDLL(path)
+    lib.lds_poison.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    from genomicsbench_palisade_amd import set_device
+    set_device(0)
+
+    def run(mode, value, seed=1):
+        st = lib.lds_poison(0, mode, value, seed)
+        assert st == 0, f"lds_poison failed: hip error {st}"
+    return run
+
+
+CHAIN_NAMES = ["scores", "parents", "targets", "peak_scores"]
+
+
+@pytest.mark.parametrize("vlanes", ["1", "0"])
+def test_chain_after_poison(poison, monkeypatch, vlanes):
+    """chain_rows (two calls per wave, stamp rings) and the speculative split path (verify_lanes, or
+    verify_kernel alone with GB_CHAIN_VLANES=0) on calls long enough to be split into segments."""
+    from genomicsbench_palisade_amd import chain
+    monkeypatch.setenv("GB_CHAIN_VLANES", vlanes)
+    calls = gen.chain_dataset("small", num_calls=400, seed=21, median_n=1500, max_n=40000)
+    exp = oracle_lib.chain_oracle(calls, 8)
+    b = chain.ChainBatch(calls)
+    try:
+        for mode, value in PATTERNS:
+            poison(mode, value)
+            b.run()
+            got = b.results()
+            for k, name in enumerate(CHAIN_NAMES):
+                bad = np.nonzero(got[k] != exp[k])[0]
+                assert len(bad) == 0, f"pattern {(mode, value)}: {name} differs at {len(bad)} anchors, first {bad[:5]}"
+            assert got[4] == exp[4], f"pattern {(mode, value)}: visited {got[4]} vs {exp[4]}"
+            assert b.split_stats()[0] > 0  # the split path ran
+    finally:
+        b.close()
+
+
+def test_fmi_search_after_poison(poison, tmp_path):
+    from genomicsbench_palisade_amd import fmi
+    ref = gen.fmi_reference(300_000, seed=31)
+    codes, lens = gen.fmi_reads(ref, 6000, read_len=151, seed=131, sub_rate=0.02, n_rate=0.002)
+    p = str(tmp_path / "r.bwt.2bit.64")
+    oi = fmi_util.OracleIndex(ref, path_out=p)
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512)
+    idx = fmi.Index.load(p)
+    rs = fmi.Reads(idx, codes, lens)
+    try:
+        for mode, value in PATTERNS:
+            poison(mode, value)
+            rs.search(19)
+            sm, tot, bc, pc = rs.results(batch_size=512)
+            assert tot == len(exp) and (bc == ebc).all() and (pc == epc).all(), f"pattern {(mode, value)}"
+            for f in ("rid", "m", "n", "k", "l", "s"):
+                assert (sm[f] == exp[f]).all(), f"pattern {(mode, value)}: field {f}"
+            assert rs.timing()[2] == oi.bwt_calls()
+    finally:
+        rs.close()
+        idx.close()
+        oi.close()
+
+
+def test_bsw_after_poison(poison):
+    from genomicsbench_palisade_amd import bsw
+    p = gen.bsw_pairs(30000, seed=41)
+    P = bsw.default_params()
+    exp, ocells, _ = oracle_lib.bsw_oracle(p, P, nthreads=8)
+    b = bsw.BswBatch(p, P)
+    try:
+        for mode, value in PATTERNS:
+            poison(mode, value)
+            b.run()
+            got, cells, _ = b.results()
+            bad = np.nonzero((got[:p.n] != exp[:p.n]).any(axis=1))[0]
+            assert len(bad) == 0, f"pattern {(mode, value)}: {len(bad)} pairs differ, first {bad[:5]}"
+            assert (cells[:p.n] == ocells[:p.n]).all()
+    finally:
+        b.close()

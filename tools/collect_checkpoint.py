@@ -31,12 +31,22 @@ def main():
         shutil.copy(ks[0], os.path.join(p, f"{tag}_kernel_stats.csv"))
         done.append(f"{tag}_kernel_stats.csv")
     for pre, dst in (("pmc", f"{tag}_pmc.json"), ("pmch", f"{tag}_human_pmc.json")):
+        # the box's own summary (gpu_checkpoint.sh pmcsum) is stamped against the tree that was profiled:
+        # copy it as it is. Re-summarising here would stamp whatever tree is checked out now.
+        boxed = os.path.join(g, f"pmcsum_{dst}")
+        if os.path.exists(boxed):
+            shutil.copy(boxed, os.path.join(p, dst))
+            done.append(dst)
+            continue
         fd = glob.glob(os.path.join(g, f"{pre}_fetch_{tag}", "**", "run_counter_collection.csv"), recursive=True)
         wd = glob.glob(os.path.join(g, f"{pre}_write_{tag}", "**", "run_counter_collection.csv"), recursive=True)
         if fd and wd:
+            # no box summary: summarise here, but stamp the digest of the commit named by GB_PMC_COMMIT
+            # (the profiled code; default HEAD), not of the working tree
+            env = dict(os.environ, GB_PMC_COMMIT=os.environ.get("GB_PMC_COMMIT", "HEAD"))
             subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.dirname(fd[0]),
-                            os.path.dirname(wd[0]), os.path.join(p, dst)], check=True, stdout=subprocess.DEVNULL)
-            done.append(dst)
+                            os.path.dirname(wd[0]), os.path.join(p, dst)], check=True, stdout=subprocess.DEVNULL, env=env)
+            done.append(dst + " (re-summarised, stamped at " + env["GB_PMC_COMMIT"] + ")")
     print("copied:", ", ".join(done) or "nothing")
 
 

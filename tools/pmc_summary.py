@@ -67,6 +67,22 @@ def load(d):
     return res
 
 
+def commit_digest(commit, leg=None):
+    """bench.source_digest over the kernel sources as they are in `commit` (git), not the working tree:
+    the stamp of a summary made after the profiled code has moved on."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from bench import _leg_match, digest_of
+    names = subprocess.run(["git", "-C", root, "ls-tree", "-r", "--name-only", commit], check=True,
+                           capture_output=True, text=True).stdout.split()
+    keep = [r for r in names if (r.startswith("genomicsbench_palisade_amd/csrc/")
+                                 or (r.startswith("include/") and r.endswith(".h") and r.count("/") <= 2)
+                                 or r == "Makefile") and _leg_match(r, leg)]
+    return digest_of([(r, subprocess.run(["git", "-C", root, "show", f"{commit}:{r}"], check=True,
+                                         capture_output=True).stdout) for r in keep])
+
+
 def main():
     fetch, write, dst = sys.argv[1], sys.argv[2], sys.argv[3]
     f, w = load(fetch), load(write)
@@ -89,8 +105,12 @@ def main():
                   "write_bytes": sum(wb) / max(len(wb), 1), "mean_ms_under_pmc": sum(ms) / max(len(ms), 1)}
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import LEG_SOURCES, source_digest
-    res["_code"] = source_digest()  # bench.py marks traffic from other kernel code "stale"
-    res["_code_legs"] = {leg: source_digest(leg) for leg in LEG_SOURCES}
+    commit = os.environ.get("GB_PMC_COMMIT")
+    dig = (lambda leg=None: commit_digest(commit, leg)) if commit else source_digest
+    res["_code"] = dig()  # bench.py marks traffic from other kernel code "stale"
+    res["_code_legs"] = {leg: dig(leg) for leg in LEG_SOURCES}
+    if commit:
+        res["_code_commit"] = commit
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024 per launch; fetch "
                     "scaled by the calibrated factor of the kernel's read class (tools/probes/pmc_calib.hip, "
                     "profiles/r01g_pmc_calib.txt), write exact")
