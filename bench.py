@@ -1361,6 +1361,16 @@ def bench_fmi_human(args, D, rank, world):
         t1 = time.perf_counter()
         _, ocalls, parts = oi.run_threaded(codes[:m], lens[:m], threads, collect=True)
         t_cpu = time.perf_counter() - t1
+        # reference kind: bwa v1's own mem_collect_intv (tools/bwa, compiled unmodified into oracle/_ref)
+        # over a bwt_t rebuilt from the same CP_OCC tables, on the same reads
+        ref_t = ref_tot = None
+        blib = fmi_util.ref_bwa()
+        if blib is not None:
+            bwt = fmi_util.bwa_from_tables(blib, n_, s_, oi._occ)
+            t1 = time.perf_counter()
+            ref_tot = fmi_util.bwa_collect_threaded(blib, bwt, codes[:m], lens[:m], threads)
+            ref_t = time.perf_counter() - t1
+            blib.ref_bwa_free(bwt)
         oi.close()
         r2 = fmi.Reads(idx, codes[:m], lens[:m])
         r2.search(19)
@@ -1375,6 +1385,13 @@ def bench_fmi_human(args, D, rank, world):
         cpu = {"value": m / t_cpu / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "port",
                "sample": f"first {m} reads, C restatement of bwa-mem2 FMI_search over the same CP_OCC tables "
                          f"(batches of 512 over {threads} threads), {t_cpu:.1f} s"}
+        if ref_t is not None:
+            if ref_tot != tot:
+                raise SystemExit(f"fmi human: bwa v1 interval count {ref_tot} != GPU SMEM count {tot}")
+            cpu = {"value": m / ref_t / 1e6, "unit": "Mreads/s", "cores": threads, "kind": "reference",
+                   "sample": f"first {m} reads, bwa v1 mem_collect_intv (tools/bwa bwt_smem1 + bwt_seed_strategy1, "
+                             f"compiled unmodified) over a bwt_t rebuilt from the same CP_OCC tables, {threads} "
+                             f"threads, {ref_t:.1f} s; {ref_tot} intervals == GPU SMEM count", "port": cpu}
     idx.close()
     return {
         "value": round(mreads, 3), "unit": "Mreads/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),

@@ -728,7 +728,10 @@ __device__ __forceinline__ void phmm_stack2(const Stack &S, const uint32_t *__re
   }
 }
 
-__global__ __launch_bounds__(64) void phmm_forward2(const Stack *__restrict__ stacks,
+// W: the waves per SIMD the register allocation is held to (0: the compiler's own choice)
+template <int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W ? W : 1, 8))) void phmm_forward2(
+                                                     const Stack *__restrict__ stacks,
                                                      const uint32_t *__restrict__ stk_tc,
                                                      const TcDesc *__restrict__ descs,
                                                      const uint8_t *__restrict__ pool, DevTab<float> tab,
@@ -840,7 +843,7 @@ int get_device_tables(DeviceTables **out) {
   st = upload_tables(*g_hd, &t->d);
   if (st) return st;
   for (auto fn : {(const void *)phmm_forward<float, false>, (const void *)phmm_forward<double, true>,
-                  (const void *)phmm_forward2})
+                  (const void *)phmm_forward2<0>, (const void *)phmm_forward2<6>, (const void *)phmm_forward2<8>})
     GB_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   g_dev[dev] = t;
   *out = t;
@@ -912,6 +915,7 @@ struct gb_phmm_batch {
   bool ran = false;
   bool force_f64 = false;
   int rpl = 2;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=1: one, for A/B probes)
+  int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
 };
 
 extern "C" {
@@ -1114,6 +1118,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   for (int k = 0; k < n; k++) total_rows += (int64_t)(desc[k].dims & 0xffff) + 2;
   b->rpl = 2;
   if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 1 ? 1 : 2;  // probes: one row per lane
+  b->w2 = 0;
+  if (const char *e = getenv("GB_PHMM_W2")) b->w2 = atoi(e);
   int stack_rows = kStackRows;
   while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
@@ -1243,15 +1249,53 @@ int batch_new(DeviceTables *tabs, gb_phmm_batch **out) {
 // reference's once-per-batch computelikelihoodsboth does not create streams, events and buffers
 // each time. Kept for the life of the thread's process (never freed: freeing at thread exit could
 // run after the HIP runtime is torn down).
-gb_phmm_batch *thread_workspace(DeviceTables *tabs, int *st) {
-  thread_local std::unordered_map<int, gb_phmm_batch *> ws;
-  auto it = ws.find(tabs->device);
-  if (it != ws.end()) return it->second;
+gb_phmm_batch *thread_workspace(DeviceTables *tabs, int *st, int slot = 0) {
+  thread_local std::unordered_map<int, std::vector<gb_phmm_batch *>> ws;
+  auto &v = ws[tabs->device];
+  if ((int)v.size() <= slot) v.resize(slot + 1, nullptr);
+  if (v[slot]) return v[slot];
   gb_phmm_batch *b = nullptr;
   *st = batch_new(tabs, &b);
   if (*st) return nullptr;
-  ws[tabs->device] = b;
+  v[slot] = b;
   return b;
+}
+
+// Pipelined one-call path for big calls: the testcases are cut into contiguous chunks, each packed
+// into its own workspace batch (own stream) and launched as soon as it is packed, so packing chunk
+// c + 1 on the host overlaps the kernels of chunk c, and chunk c's results (D2H + log10) overlap the
+// kernels of the chunks after it. Chunks are independent jobs, so results are those of one job.
+constexpr int kPipeMinChunk = 65536;  // testcases per chunk at least
+constexpr int kPipeMaxChunks = 4;
+
+int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double *results, float *raw_f,
+                      double *raw_d, uint8_t *used_double) {
+  const char *e = getenv("GB_PHMM_PIPE");  // probes: the chunk count (1 = one job, no overlap)
+  int k = std::min(kPipeMaxChunks, std::max(1, n / kPipeMinChunk));
+  if (e) k = std::max(1, std::min(16, atoi(e)));
+  std::vector<gb_phmm_batch *> B(k);
+  std::vector<int> lo(k + 1);
+  for (int c = 0; c <= k; c++) lo[c] = (int)((int64_t)n * c / k);
+  int st = GB_OK;
+  for (int c = 0; c < k; c++) {
+    B[c] = thread_workspace(tabs, &st, c);
+    if (!B[c]) return st;
+    B[c]->force_f64 = false;
+  }
+  HostClock clk;
+  auto fetch = [&](int c) {
+    const int o = lo[c];
+    return gb_phmm_batch_results(B[c], results ? results + o : nullptr, raw_f ? raw_f + o : nullptr,
+                                 raw_d ? raw_d + o : nullptr, used_double ? used_double + o : nullptr, nullptr);
+  };
+  for (int c = 0; c < k; c++) {
+    if ((st = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c]))) return st;
+    if ((st = gb_phmm_batch_run(B[c]))) return st;
+    if (c > 0 && (st = fetch(c - 1))) return st;
+  }
+  st = fetch(k - 1);
+  clk.mark("pipelined compute");
+  return st;
 }
 
 }  // namespace
@@ -1296,7 +1340,8 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
       if (ns > 0 && b->rpl == 2) {
         const size_t lds_f2 = sizeof(Brec<float>) * (size_t)(b->max_haplen + kBndPad2 + kRecPad) +
                               (size_t)(b->max_haplen + kBndPad2 + kCodePad2) + 16;
-        hipLaunchKernelGGL(phmm_forward2, dim3(ns), dim3(kWave), lds_f2, b->stream, b->d_stacks, b->d_stk_tc,
+        auto k2 = b->w2 == 8 ? phmm_forward2<8> : b->w2 == 6 ? phmm_forward2<6> : phmm_forward2<0>;
+        hipLaunchKernelGGL(k2, dim3(ns), dim3(kWave), lds_f2, b->stream, b->d_stacks, b->d_stk_tc,
                            b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf);
       } else if (ns > 0) {
         hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
@@ -1436,6 +1481,8 @@ int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f
   DeviceTables *tabs = nullptr;
   int st = get_device_tables(&tabs);
   if (st) return st;
+  if (n >= 2 * kPipeMinChunk || getenv("GB_PHMM_PIPE"))
+    return compute_pipelined(tabs, tcs, n, results, raw_f, raw_d, used_double);
   gb_phmm_batch *b = thread_workspace(tabs, &st);
   if (!b) return st;
   b->force_f64 = false;

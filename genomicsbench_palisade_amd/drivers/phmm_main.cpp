@@ -97,18 +97,26 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
         t.c = r.c.c_str();
         tcs.push_back(t);
       }
-  gb_phmm_batch *job = nullptr;
-  st = gb_phmm_batch_create(tcs.data(), (int)tcs.size(), &job);
-  if (st) die("gb_phmm_batch_create", st);
   std::vector<double> res(tcs.size());
-  for (int l = 0; l < loops; l++) {
-    st = gb_phmm_batch_run(job);
-    if (st) die("gb_phmm_batch_run", st);
+  if (loops == 1) {
+    // one pass: gb_phmm_compute pipelines big jobs (packing chunk c + 1 while chunk c computes)
+    st = gb_phmm_compute(tcs.data(), (int)tcs.size(), res.data(), nullptr, nullptr, nullptr);
+    if (st) die("gb_phmm_compute", st);
+    gettimeofday(&t1, nullptr);
+  } else {
+    // -l N: the job is packed once and stays on the device for the N passes
+    gb_phmm_batch *job = nullptr;
+    st = gb_phmm_batch_create(tcs.data(), (int)tcs.size(), &job);
+    if (st) die("gb_phmm_batch_create", st);
+    for (int l = 0; l < loops; l++) {
+      st = gb_phmm_batch_run(job);
+      if (st) die("gb_phmm_batch_run", st);
+    }
+    st = gb_phmm_batch_results(job, res.data(), nullptr, nullptr, nullptr, nullptr);
+    if (st) die("gb_phmm_batch_results", st);
+    gettimeofday(&t1, nullptr);
+    gb_phmm_batch_destroy(job);
   }
-  st = gb_phmm_batch_results(job, res.data(), nullptr, nullptr, nullptr, nullptr);
-  if (st) die("gb_phmm_batch_results", st);
-  gettimeofday(&t1, nullptr);
-  gb_phmm_batch_destroy(job);
   size_t k = 0;
   for (Batch *b : shard)
     for (auto &v : b->results) v = res[k++];

@@ -123,18 +123,51 @@ void *ref_bwa_from_cp_occ(const int64_t *cp_occ, int64_t n, int64_t sentinel) {
   bwt->primary = (bwtint_t)sentinel;
   bwt->seq_len = seq_len;
   bwt->bwt_size = (seq_len + 15) >> 4;
-  bwt->bwt = (uint32_t *)calloc(bwt->bwt_size, 4);
-  for (int64_t row = 0, k = 0; row < n; row++) {
-    if (row == sentinel) continue;
-    const int64_t *line = cp_occ + (row >> 6) * 8;
-    const uint64_t bit = 1ull << (63 - (row & 63));
-    uint32_t b = 0;
-    for (int x = 1; x < 4; x++)
-      if ((uint64_t)line[4 + x] & bit) b = (uint32_t)x;
-    c[b]++;
-    bwt->bwt[k >> 4] |= b << ((~k & 0xf) << 1);
-    k++;
+  /* word-level packing (a human-scale index has 6.4 G rows): per 64-row line the code bits
+   * hi = G|T, lo = C|T, interleaved MSB-first into two 64-bit words = four bwt words of 16 bases;
+   * the sentinel row (code 0 here) is then cut out by shifting the rest of the array left by one
+   * base. Equal to the row-by-row packing (tests/test_fmi_oracle.py). */
+  const int64_t nlines = (n + 63) >> 6, nw = nlines * 4 + 2;
+  uint32_t *w = (uint32_t *)calloc((size_t)nw, 4);
+  for (int64_t ln = 0; ln < nlines; ln++) {
+    const uint64_t *line = (const uint64_t *)(cp_occ + ln * 8);
+    uint64_t valid = ~0ull;
+    if ((ln << 6) + 64 > n) valid = ~0ull << (64 - (n - (ln << 6)));
+    const uint64_t m1 = line[5] & valid, m2 = line[6] & valid, m3 = line[7] & valid;
+    const uint64_t hi = m2 | m3, lo = m1 | m3;
+    for (int half = 0; half < 2; half++) {
+      /* 32 rows: bits 63..32 (half 0) or 31..0 (half 1) of hi / lo, row order MSB-first */
+      uint64_t h = (hi >> (32 * (1 - half))) & 0xffffffffull, l = (lo >> (32 * (1 - half))) & 0xffffffffull;
+      /* spread 32 bits to the even positions of 64 */
+      h = (h | (h << 16)) & 0x0000FFFF0000FFFFull; h = (h | (h << 8)) & 0x00FF00FF00FF00FFull;
+      h = (h | (h << 4)) & 0x0F0F0F0F0F0F0F0Full; h = (h | (h << 2)) & 0x3333333333333333ull;
+      h = (h | (h << 1)) & 0x5555555555555555ull;
+      l = (l | (l << 16)) & 0x0000FFFF0000FFFFull; l = (l | (l << 8)) & 0x00FF00FF00FF00FFull;
+      l = (l | (l << 4)) & 0x0F0F0F0F0F0F0F0Full; l = (l | (l << 2)) & 0x3333333333333333ull;
+      l = (l | (l << 1)) & 0x5555555555555555ull;
+      const uint64_t v = (h << 1) | l; /* row 32*half + j at bits 63-2j, 62-2j */
+      w[ln * 4 + 2 * half] = (uint32_t)(v >> 32);
+      w[ln * 4 + 2 * half + 1] = (uint32_t)v;
+    }
+    c[1] += (uint64_t)__builtin_popcountll(m1 & ~m2 & ~m3);
+    c[2] += (uint64_t)__builtin_popcountll(m2 & ~m3);
+    c[3] += (uint64_t)__builtin_popcountll(m3);
   }
+  c[0] = (bwtint_t)(n - 1) - c[1] - c[2] - c[3];
+  /* drop the sentinel's base: every base after it moves one place (2 bits) towards the front */
+  {
+    const int64_t wk = sentinel >> 4;
+    const int sh = (int)(sentinel & 15);
+    const uint32_t keep = sh ? ~0u << (32 - 2 * sh) : 0u; /* bases before the sentinel in its word */
+    uint32_t cur = w[wk];
+    w[wk] = (cur & keep) | ((cur << 2) & ~keep) | (w[wk + 1] >> 30);
+    for (int64_t k = wk + 1; k + 1 < nw; k++) w[k] = (w[k] << 2) | (w[k + 1] >> 30);
+  }
+  bwt->bwt = (uint32_t *)calloc(bwt->bwt_size, 4);
+  memcpy(bwt->bwt, w, (size_t)bwt->bwt_size * 4);
+  free(w);
+  /* the row-by-row form this replaces left every bit past seq_len zero */
+  if (seq_len & 15) bwt->bwt[bwt->bwt_size - 1] &= ~0u << (32 - 2 * (seq_len & 15));
   bwt->L2[0] = 0;
   for (int x = 0; x < 4; x++) bwt->L2[x + 1] = bwt->L2[x] + c[x];
   bwt_bwtupdate_core(bwt);

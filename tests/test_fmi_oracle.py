@@ -147,14 +147,16 @@ def test_sa_oracle_vs_bwa_live(tmp_path):
     assert (oi.sa_lookup(np.arange(n), 0) == exp).all()
 
 
-def test_bwa_v1_over_cp_occ_tables_matches_oracle(tmp_path):
+@pytest.mark.parametrize("size,seed", [(120_000, 21), (1_000, 3), (4_099, 4), (65_553, 5)])
+def test_bwa_v1_over_cp_occ_tables_matches_oracle(tmp_path, size, seed):
     """bwa v1's own SMEM collection (mem_collect_intv over bwt_smem1/bwt_seed_strategy1) running on a
     bwt_t rebuilt from bwa-mem2 CP_OCC tables equals the oracle per read -- this is what makes it a
-    'reference'-kind CPU baseline over the GPU-built index."""
+    'reference'-kind CPU baseline over the GPU-built index. Sizes put the sentinel row and the table's
+    end at different places of the 16-base words the word-level packing writes."""
     lib = fmi_util.ref_bwa()
     if lib is None:
         pytest.skip("oracle/_ref/libref_bwa.so not built")
-    ref = gen.fmi_reference(120_000, seed=21, repeat_frac=0.2)
+    ref = gen.fmi_reference(size, seed=seed, repeat_frac=0.2)
     p = str(tmp_path / "o.bwt.2bit.64")
     oi = fmi_util.OracleIndex(ref, path_out=p)
     n, _, sent = oi.info()
@@ -162,7 +164,7 @@ def test_bwa_v1_over_cp_occ_tables_matches_oracle(tmp_path):
     sz = (n >> 6) + 1
     cp = raw[48:48 + sz * 64].view(np.int64).reshape(sz, 8)
     bwt = fmi_util.bwa_from_tables(lib, n, sent, cp)
-    codes, lens = gen.fmi_reads(ref, 600, seed=22, sub_rate=0.02)
+    codes, lens = gen.fmi_reads(ref, 600, seed=seed + 1, read_len=min(151, size // 4), sub_rate=0.02)
     got = fmi_util.bwa_smems(lib, bwt, codes, lens)
     exp, _, _ = oi.run(codes, lens, batch_size=512)
     assert got == fmi_util.per_read(exp, len(lens))

@@ -174,3 +174,28 @@ def test_stack_edges_vs_oracle(phmm, seed):
     exp = oracle_run(ta)
     assert_exact(got, exp)
     assert (got[3].astype(bool) == exp[3].astype(bool)).all()
+
+
+@pytest.mark.parametrize("chunks", ["3", "1"])
+def test_pipelined_compute_bit_exact(phmm, monkeypatch, chunks):
+    """gb_phmm_compute's pipelined path (chunks packed and launched one after the other on their own
+    streams; GB_PHMM_PIPE forces it for a small call) gives the one-job results, against the oracle."""
+    monkeypatch.setenv("GB_PHMM_PIPE", chunks)
+    rng = np.random.default_rng(23)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(5)])
+    got = phmm.compute_likelihoods_both(ta)
+    assert_exact(got, oracle_run(ta))
+    assert (got[3].astype(bool) == (got[1] < np.float32(1e-28))).all()
+
+
+def test_rows_per_lane_ab_identical(phmm, monkeypatch):
+    """The f32 pass with two rows per lane (default) and with one (GB_PHMM_RPL=1) agree bit for bit
+    on a job with many stacks, partial stripes and both passes."""
+    rng = np.random.default_rng(29)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 50, 20) for _ in range(4)])
+    outs = []
+    for rpl in ("1", "2"):
+        monkeypatch.setenv("GB_PHMM_RPL", rpl)
+        outs.append(phmm.compute_likelihoods_both(ta))
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert (bits(a) == bits(b)).all()

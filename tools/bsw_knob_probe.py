@@ -16,9 +16,12 @@ if os.environ.get("BSW_LIB"):  # another build of libgb.so, to time two builds o
     g.LIBGB = os.path.abspath(os.environ["BSW_LIB"])
 from genomicsbench_palisade_amd import bsw, gen, set_device, shard  # noqa: E402
 
-KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP", "GB_BSW_QSHIFT", "GB_BSW_KEYORD")
+KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP", "GB_BSW_QSHIFT", "GB_BSW_KEYORD",
+         "GB_BSW_TAIL", "GB_BSW_LONG")
 set_device(0)
-pairs = gen.bsw_dataset(seed=11, threads=16)
+# BSW_PAIRS: the set size (default the 'large' set; gen.BSW_SMALL_PAIRS for 'small')
+pairs = gen.bsw_dataset(int(os.environ["BSW_PAIRS"]), seed=11, threads=16) if os.environ.get("BSW_PAIRS") \
+    else gen.bsw_dataset(seed=11, threads=16)
 sets = [("large", pairs)]
 if os.environ.get("BSW_SHARD", "1") == "1":
     sets.append(("shard0/8", shard.shard_pairs(pairs, 0, 8)[0]))

@@ -4,6 +4,7 @@ CHAIN_CONFIGS (';'-separated, each a ','-free list of VAR=VALUE joined by '+', '
 Per set and setting: batch-event ms per step (best of 10 after 3 warm-ups), Manchors/s, split
 statistics and whether every output equals the default setting's (bit for bit)."""
 import os
+import re
 import sys
 
 import numpy as np
@@ -21,13 +22,26 @@ sets = [("shard0/8", shard.shard_calls(large, 0, 8)[0]), ("large", large)]
 if os.environ.get("CHAIN_SETS"):
     sets = [s for s in sets if s[0] in os.environ["CHAIN_SETS"].split(",")]
 configs = os.environ.get("CHAIN_CONFIGS", "").split(";")
-KNOBS = ("GB_CHAIN_SPLIT", "GB_CHAIN_ROWS", "GB_CHAIN_ROWS_MAXN", "GB_CHAIN_VLANES", "GB_CHAIN_PRIO")
+KNOBS = ("GB_CHAIN_SPLIT", "GB_CHAIN_ROWS", "GB_CHAIN_ROWS_MAXN", "GB_CHAIN_VLANES", "GB_CHAIN_PRIO", "GB_CHAIN_SPREAD",
+         "GB_CHAIN_EXP")
+
+
+def parse_cfg(cfg):
+    """'VAR=VALUE+VAR=VALUE' -> ['VAR=VALUE', ...]; a '+' only separates settings when a knob name
+    follows it, and anything else is refused with the offending setting named (round 4's probe died
+    with a bare ValueError on a malformed setting, profiles/r04zj_chain_warm_ab.log)."""
+    parts = [c for c in re.split(r"\+(?=GB_)", cfg) if c]
+    for kv in parts:
+        if "=" not in kv or kv.split("=", 1)[0] not in KNOBS:
+            raise SystemExit(f"chain_knob_probe: bad setting {kv!r} in CHAIN_CONFIGS entry {cfg!r} "
+                             f"(want VAR=VALUE with VAR one of {', '.join(KNOBS)})")
+    return parts
 
 
 def run(calls, cfg):
     for k in KNOBS:
         os.environ.pop(k, None)
-    for kv in [c for c in cfg.split("+") if c]:
+    for kv in parse_cfg(cfg):
         k, v = kv.split("=", 1)
         os.environ[k] = v
     b = chain.ChainBatch(calls)
