@@ -461,6 +461,8 @@ def headline(line: dict, detail_path=None) -> dict:
                             "speedup": _sig(sp.get("projected_speedup"))}
     if isinstance(line.get("roofline_f64"), dict):
         h["roofline_f64_frac"] = _sig(line["roofline_f64"].get("frac"))
+    if line.get("f32_only_gcups"):
+        h["f32_only_gcups"] = _sig(line["f32_only_gcups"])
     for leg in ("fmi", "chain", "bsw"):
         h[leg] = _leg_short(line.get(leg))
     fm, ch = line.get("fmi") or {}, line.get("chain") or {}
@@ -1162,6 +1164,9 @@ def bench_phmm(args, D, rank, world, kind="large"):
                   if args.scaling == "strong" and world > 1 else shard_note(args, "testcases", 0, full.n, full.n, world)),
         "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
+        # the f32 pass alone over every cell: what the step would be without the f64 fallback (its
+        # 36 % share of testcases is a property of the synthetic generator)
+        "f32_only_gcups": cells / max(ms32 * 1e-3, 1e-12) / 1e9,
     }
     if world > 1:
         def full_pass(w):
@@ -1798,6 +1803,7 @@ def main():
             "kernels_ms": ph["kernels_ms"] if ph else None,
             "shard_proxy": ph.get("shard_proxy") if ph else None,
             "rank_check": ph.get("rank_check") if ph else None,
+            "f32_only_gcups": ph.get("f32_only_gcups") if ph else None,
             "cpu_baseline": ph["cpu_baseline"] if ph else None,
             "dropin_e2e": ph.get("dropin_e2e") if ph else None,
             "fmi": fm,
