@@ -638,14 +638,26 @@ __global__ __launch_bounds__(64) void bsw_seg_kernel(SegArgs A) {
     int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
     int ncells = 0;
     bool active = valid && tlen > 0;
-    uint32_t tnext = active ? tgt[0] : 0u;
+    // target bases 64 rows at a time: lane s of the row holds bases [i0 + 4s, i0 + 4s + 4), and a row
+    // takes its base from that lane with one ds_bpermute, so no row waits on a global load (a byte
+    // load issued a row ahead was exposed: a row here is far shorter than a pair-per-lane row)
+    const int sbase = lane & ~(kSegLanes - 1);
+    uint32_t tword = 0;
 #pragma unroll 1
     for (int i = 0;; ++i) {
       if (i >= tlen) active = false;
       if (__builtin_amdgcn_ballot_w64(active) == 0) break;
       if (!active) continue;
-      const uint32_t tb = min(tnext, 4u);
-      tnext = tgt[min(i + 1, tlen - 1)];  // next row's base, a row ahead
+      if ((i & 63) == 0) {
+        tword = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int t = i + 4 * s + b;
+          if (t < tlen) tword |= (uint32_t)tgt[t] << (8 * b);
+        }
+      }
+      const uint32_t tw = (uint32_t)__shfl((int)tword, sbase + ((i & 63) >> 2));
+      const uint32_t tb = min((tw >> (8 * (i & 3))) & 0xFFu, 4u);
       const uint32_t tlo = tab[2 * tb], thi = tab[2 * tb + 1];
       // band (bandedSWA.cpp:180-182)
       if (beg < i - w) beg = i - w;
@@ -982,11 +994,15 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // pair-per-lane lane's time. Both cuts rank the lane pairs by rows x chunks.
   {
     const char *te = getenv("GB_BSW_TAIL");
-    const double frac = te ? atof(te) : 0.1;  // r03ab, 100 k pairs: 0 228, 0.05 234, 0.1 258, 0.2 243 GCUPS
+    // r03ab, 100 k pairs: 0 228, 0.05 234, 0.1 258, 0.2 243 GCUPS. A batch of fewer lane waves than
+    // SIMDs (the 1/8 shard of the 'small' set: 12.5 k pairs, 195 waves on 1 024 SIMDs) is one wave's
+    // critical path long: every lane pair goes to the wave-per-pair kernel (1.30 -> 0.56 ms,
+    // profiles/r05b_bsw_small.log)
+    const double frac = te ? atof(te) : (n < (int64_t)64 * 4 * std::max(B->num_cus, 1) ? 1.0 : 0.1);
     const char *se = getenv("GB_BSW_SEG");
     const double sfrac = se ? atof(se) : 0.0;
     const int64_t fill = (int64_t)64 * 8 * std::max(B->num_cus, 1);  // lane waves of 64 pairs, 2 per SIMD
-    if ((frac > 0 || sfrac > 0) && n >= 1024 && n <= 2 * fill) {
+    if ((frac > 0 || sfrac > 0) && (n >= 1024 || frac >= 1.0) && n <= 2 * fill) {
       auto cost_of = [&](int64_t p) { return (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)); };
       std::vector<uint32_t> cost;
       cost.reserve((size_t)n);

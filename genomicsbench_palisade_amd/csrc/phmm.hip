@@ -914,7 +914,7 @@ struct gb_phmm_batch {
   int cus = 256;                   // compute units of the device (stack height rule)
   bool ran = false;
   bool force_f64 = false;
-  int rpl = 2;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=1: one, for A/B probes)
+  int rpl = 1;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=2: two, for A/B probes)
   int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
 };
 
@@ -1116,8 +1116,11 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   // 256 4.64 per step; on the whole job 2048 rows stay best (33.0 ms; 512: 33.7).
   int64_t total_rows = 0;
   for (int k = 0; k < n; k++) total_rows += (int64_t)(desc[k].dims & 0xffff) + 2;
-  b->rpl = 2;
-  if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 1 ? 1 : 2;  // probes: one row per lane
+  // one row per lane: the two-row form (phmm_forward2) issues 125 VALU per 8 cells against 67 per 4
+  // but measured slower at every register budget (f32 19.1 ms; two rows 19.8 / 20.6 / 20.9 ms at 5 /
+  // 6 / 8 waves per SIMD, profiles/r05b_phmm_rpl_ab.log); GB_PHMM_RPL=2 selects it for A/B probes
+  b->rpl = 1;
+  if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 2 ? 2 : 1;
   b->w2 = 0;
   if (const char *e = getenv("GB_PHMM_W2")) b->w2 = atoi(e);
   int stack_rows = kStackRows;

@@ -99,7 +99,12 @@ def _gpu(p, P):
 
 
 @pytest.mark.gpu
-def test_gpu_vs_golden(golden):
+@pytest.mark.parametrize("tail", ["0", None])
+def test_gpu_vs_golden(golden, monkeypatch, tail):
+    """tail "0": every pair on the pair-per-lane kernels; None: the default routing (a batch this
+    small runs on the wave-per-pair kernel)."""
+    if tail is not None:
+        monkeypatch.setenv("GB_BSW_TAIL", tail)
     p, sets = golden
     for name, (P, exp) in sets.items():
         got, cells, tot = _gpu(p, P)
@@ -112,7 +117,10 @@ def test_gpu_vs_golden(golden):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,n,qlen,extra", [(1, 100000, (10, 150), (0, 100)), (2, 20000, (150, 255), (0, 400)),
                                                (3, 20000, (1, 70), (0, 1500))])
-def test_gpu_vs_oracle(seed, n, qlen, extra):
+@pytest.mark.parametrize("tail", ["0", None])
+def test_gpu_vs_oracle(seed, n, qlen, extra, tail, monkeypatch):
+    if tail is not None:
+        monkeypatch.setenv("GB_BSW_TAIL", tail)
     p = gen.bsw_pairs(n, seed=seed, qlen=qlen, extra=extra)
     P = bsw.default_params()
     got, cells, tot = _gpu(p, P)
@@ -129,6 +137,7 @@ def test_gpu_grouping_key_does_not_change_results(monkeypatch, h0step, qshift):
     the caller's order (pairs with h0 0, large h0 and every variant in the set)."""
     monkeypatch.setenv("GB_BSW_H0STEP", h0step)
     monkeypatch.setenv("GB_BSW_QSHIFT", qshift)
+    monkeypatch.setenv("GB_BSW_TAIL", "0.1")  # the lane kernels (a batch this small would go to the wave kernel)
     p = gen.bsw_pairs(30000, seed=17, qlen=(1, 160), extra=(0, 200))
     p.h0[::7] = 0
     p.h0[1::11] = 200

@@ -88,8 +88,12 @@ def test_fmi_search_after_poison(poison, tmp_path):
         oi.close()
 
 
-def test_bsw_after_poison(poison):
+@pytest.mark.parametrize("tail", ["0", "1"])
+def test_bsw_after_poison(poison, monkeypatch, tail):
+    """tail "0": the pair-per-lane kernels (bsw_lane_kernel's LDS query codes and per-lane constants),
+    "1": the wave-per-pair kernel."""
     from genomicsbench_palisade_amd import bsw
+    monkeypatch.setenv("GB_BSW_TAIL", tail)
     p = gen.bsw_pairs(30000, seed=41)
     P = bsw.default_params()
     exp, ocells, _ = oracle_lib.bsw_oracle(p, P, nthreads=8)

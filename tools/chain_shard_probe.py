@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 from genomicsbench_palisade_amd import chain, gen, set_device, shard  # noqa: E402
 
 set_device(0)
-full = gen.chain_dataset("large", seed=5)
+full = gen.chain_dataset(os.environ.get("CHAIN_KIND", "large"), seed=5)  # CHAIN_KIND=small: the 'small' set
 of, r = int(os.environ.get("CHAIN_OF", "8")), int(os.environ.get("CHAIN_RANK", "0"))
 calls, (lo, hi) = shard.shard_calls(full, r, of) if of > 1 else (full, (0, full.ncalls))
 print(f"shard {r}/{of}: calls {lo}..{hi}, {calls.nanchors} anchors", flush=True)
