@@ -541,229 +541,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Segment-per-pair kernel (latency path for small batches and for the long pairs of a batch that
-// fills the chip only once): one pair per 16-lane DPP row, four pairs per wave, K columns per lane
-// (16 K >= qlen + 1). A pair-per-lane wave's critical path is one lane sweeping its whole pair
-// (rows x 8 NCH columns one after another, ~1.4 ms for 250 x 160 under a short grid); here a row is
-// K columns per lane plus the segment's collectives, and the chip holds 16x more waves for the same
-// pairs. The row is extend<K>'s (the same recurrences and bookkeeping, bandedSWA.cpp:130-251), with
-// every wave-wide scan / reduction / readlane replaced by its 16-lane DPP row form: row_shr for the
-// F prefix scan and the one-column shift, row_ror rotations for all-reduces (each lane of the row
-// ends with the row's value), so the four pairs of a wave never see each other's lanes.
-constexpr int kSegLanes = 16;
-
-template <int CTRL>
-__device__ __forceinline__ int dpp_row(int old, int v) {
-  return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int seg_scan_max(int v) {  // inclusive, within the 16-lane row
-  v = max(v, dpp_row<0x111>(kNeg, v));
-  v = max(v, dpp_row<0x112>(kNeg, v));
-  v = max(v, dpp_row<0x114>(kNeg, v));
-  v = max(v, dpp_row<0x118>(kNeg, v));
-  return v;
-}
-__device__ __forceinline__ int seg_max(int v) {  // all-reduce: row_ror 8, 4, 2, 1
-  v = max(v, dpp_row<0x128>(v, v));
-  v = max(v, dpp_row<0x124>(v, v));
-  v = max(v, dpp_row<0x122>(v, v));
-  v = max(v, dpp_row<0x121>(v, v));
-  return v;
-}
-__device__ __forceinline__ int seg_min(int v) {
-  v = min(v, dpp_row<0x128>(v, v));
-  v = min(v, dpp_row<0x124>(v, v));
-  v = min(v, dpp_row<0x122>(v, v));
-  v = min(v, dpp_row<0x121>(v, v));
-  return v;
-}
-
-struct SegArgs {
-  const Pair *pairs;
-  const uint32_t *list;  // order[first .. first + count)
-  int64_t count;
-  const uint8_t *tgt, *qry;
-  int32_t *out6, *cells;
-  unsigned long long *total_cells;
-  unsigned int *next;  // groups of four pairs handed out to waves
-  int o_del, e_del, o_ins, e_ins, zdrop;
-  uint32_t tab[10];  // as LaneArgs::tab
-};
-
-template <int K>
-__global__ __launch_bounds__(64) void bsw_seg_kernel(SegArgs A) {
-  __shared__ uint32_t tab[10];
-  if (threadIdx.x < 10) tab[threadIdx.x] = A.tab[threadIdx.x];
-  __syncthreads();
-  const int lane = threadIdx.x;
-  const int s = lane & (kSegLanes - 1);  // lane in the pair's row
-  const int o_del = A.o_del, e_del = A.e_del, o_ins = A.o_ins, e_ins = A.e_ins;
-  const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
-  constexpr int NQ = (K + 3) / 4;
-  for (;;) {
-    unsigned int g = 0;
-    if (lane == 0) g = atomicAdd(A.next, 1u);
-    g = (unsigned int)__builtin_amdgcn_readfirstlane((int)g);
-    if ((int64_t)g * 4 >= A.count) break;
-    const int64_t k = (int64_t)g * 4 + (lane >> 4);
-    const bool valid = k < A.count;
-    const uint32_t p = valid ? A.list[k] : 0u;
-    Pair P;
-    if (valid) {
-      P = A.pairs[p];
-    } else {
-      P.t_off = P.q_off = 0;
-      P.tlen = 0;
-      P.qlen = 1;
-      P.h0 = 0;
-      P.w = 0;
-    }
-    const int qlen = P.qlen, tlen = P.tlen, h0 = P.h0, w = P.w;
-    const uint8_t *qry = A.qry + P.q_off;
-    const uint8_t *tgt = A.tgt + P.t_off;
-    int H[K], E[K];
-    uint32_t qw[NQ];
-    const int v1 = max(h0 - oe_ins, 0);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) qw[q] = 0;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const int j = s * K + c;
-      const uint32_t qb = j < qlen ? min((uint32_t)qry[j], 4u) : 4u;
-      qw[c >> 2] |= qb << (8 * (c & 3));
-      H[c] = j == 0 ? h0 : (j <= qlen ? max(v1 - (j - 1) * e_ins, 0) : 0);  // bandedSWA.cpp:157-159
-      E[c] = 0;
-    }
-    int beg = 0, end = qlen, mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
-    int ncells = 0;
-    bool active = valid && tlen > 0;
-    // target bases 64 rows at a time: lane s of the row holds bases [i0 + 4s, i0 + 4s + 4), and a row
-    // takes its base from that lane with one ds_bpermute, so no row waits on a global load (a byte
-    // load issued a row ahead was exposed: a row here is far shorter than a pair-per-lane row)
-    const int sbase = lane & ~(kSegLanes - 1);
-    uint32_t tword = 0;
-#pragma unroll 1
-    for (int i = 0;; ++i) {
-      if (i >= tlen) active = false;
-      if (__builtin_amdgcn_ballot_w64(active) == 0) break;
-      if (!active) continue;
-      if ((i & 63) == 0) {
-        tword = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int t = i + 4 * s + b;
-          if (t < tlen) tword |= (uint32_t)tgt[t] << (8 * b);
-        }
-      }
-      const uint32_t tw = (uint32_t)__shfl((int)tword, sbase + ((i & 63) >> 2));
-      const uint32_t tb = min((tw >> (8 * (i & 3))) & 0xFFu, 4u);
-      const uint32_t tlo = tab[2 * tb], thi = tab[2 * tb + 1];
-      // band (bandedSWA.cpp:180-182)
-      if (beg < i - w) beg = i - w;
-      if (end > i + w + 1) end = i + w + 1;
-      if (end > qlen) end = qlen;
-      const int h1init = beg == 0 ? max(h0 - (o_del + e_del * (i + 1)), 0) : 0;
-      ncells += max(end - beg, 0);
-      int M[K], lpx[K];
-      int lp = kNeg;
-      uint32_t sw = 0;  // score bytes of four columns: the row's scores looked up by their query codes
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const int j = s * K + c;
-        const bool inb = j >= beg && j < end;
-        if ((c & 3) == 0) sw = __builtin_amdgcn_perm(thi, tlo, qw[c >> 2]);
-        const int sc = (int)(int8_t)(sw >> (8 * (c & 3)));
-        M[c] = H[c] ? H[c] + sc : 0;  // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0
-        const int gv = inb ? max(M[c] - oe_ins, 0) + e_ins * j : kNeg;
-        lpx[c] = lp;
-        lp = max(lp, gv);
-      }
-      const int lex = dpp_row<0x111>(kNeg, seg_scan_max(lp));  // exclusive: the lanes to the left
-      int hm = -1, key = -1, hlast = 0;
-      int hv[K], En[K];
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const int j = s * K + c;
-        const bool inb = j >= beg && j < end;
-        const int f = max(max(lex, lpx[c]) - e_ins * j + e_ins, 0);  // F(i,j)
-        hv[c] = max(max(M[c], E[c]), f);
-        En[c] = max(max(E[c] - e_del, M[c] - oe_del), 0);  // E(i+1,j)
-        if (inb) {
-          hm = max(hm, hv[c]);
-          key = max(key, hv[c] << 16 | j);  // the last column reaching the row maximum wins
-        }
-      }
-      hlast = hv[K - 1];
-      const int m = max(seg_max(hm), 0);
-      const int kmax = seg_max(key);
-      const int mj = m > 0 ? (kmax & 0xFFFF) : -1;  // bandedSWA.cpp:203-204
-      // eh[j].h <- H(i,j-1) for j in (wlo, end], eh[wlo].h <- the first column's, eh[j].e <- E(i+1,j),
-      // eh[end].e <- 0 (bandedSWA.cpp:195-197,217)
-      const int wlo = min(beg, end);
-      const int hprev = dpp_row<0x111>(0, hlast);
-      int h1own = kNeg;
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const int j = s * K + c;
-        const int hs = c ? hv[c - 1] : hprev;
-        if (j >= wlo && j <= end) {
-          H[c] = j == wlo ? h1init : hs;
-          E[c] = j == end ? 0 : En[c];
-        }
-        if (j == end) h1own = H[c];
-      }
-      const int h1 = seg_max(h1own);
-      if ((beg < end ? end : beg) == qlen) {  // bandedSWA.cpp:218-221
-        max_ie = gscore > h1 ? max_ie : i;
-        gscore = gscore > h1 ? gscore : h1;
-      }
-      if (m == 0) {
-        active = false;
-        continue;
-      }
-      if (m > mx) {
-        mx = m, max_i = i, max_j = mj;
-        max_off = max(max_off, abs(mj - i));
-      } else if (A.zdrop > 0) {
-        const bool brk = (i - max_i > mj - max_j) ? (mx - m - ((i - max_i) - (mj - max_j)) * e_del > A.zdrop)
-                                                  : (mx - m - ((mj - max_j) - (i - max_i)) * e_ins > A.zdrop);
-        if (brk) {
-          active = false;
-          continue;
-        }
-      }
-      // band narrowing (bandedSWA.cpp:235-239): the first nonzero eh in [beg, end), the last in
-      // [nb, end] (= the last nonzero in [beg, end] when there is one: nb is at or before it)
-      int jf = INT_MAX, jl = -1;
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const int j = s * K + c;
-        const bool nz = (H[c] | E[c]) != 0;
-        if (nz && j >= beg && j < end) jf = min(jf, j);
-        if (nz && j >= beg && j <= end) jl = j;
-      }
-      jf = seg_min(jf);
-      jl = seg_max(jl);
-      const int nb = jf != INT_MAX ? jf : end;
-      const int je = jl >= nb ? jl : nb - 1;
-      beg = nb;
-      end = je + 2 < qlen ? je + 2 : qlen;
-    }
-    if (valid && s == 0) {
-      int32_t *o6 = A.out6 + 6 * (int64_t)p;
-      o6[0] = mx;
-      o6[1] = max_j + 1;
-      o6[2] = max_i + 1;
-      o6[3] = max_ie + 1;
-      o6[4] = gscore;
-      o6[5] = max_off;
-      A.cells[p] = ncells;
-      if (ncells) atomicAdd(A.total_cells, (unsigned long long)ncells);
-    }
-  }
-}
-
 // band adjustment of bandedSWA.cpp:161-170, in the reference's double arithmetic
 static int adjust_w(int w, int qlen, int mx, const gb_bsw_params &p) {
   int max_ins = (int)((double)(qlen * mx + p.end_bonus - p.o_ins) / p.e_ins + 1.);
@@ -780,9 +557,7 @@ struct gb_bsw_batch {
   int device = -1, num_cus = 0;
   // launch plan: order[seg[v] .. seg[v+1]) are the pairs of variant v (lane kernels NCH = 4, 8, 12,
   // 16, 20; v = 5: wave-per-pair kernel), each segment sorted by decreasing target length
-  // 16, 20; v = 5: wave-per-pair kernel; v = 6..10: segment-per-pair kernel, K = 2 (v - 5) columns
-  // per lane)
-  static constexpr int kVariants = 11;
+  static constexpr int kVariants = 6;
   int64_t seg[kVariants + 1] = {0};
   uint32_t *d_order = nullptr;
   unsigned long long *d_prof = nullptr;  // GB_BSW_PROF=1 per-variant sweep counters (development aid)
@@ -797,8 +572,8 @@ struct gb_bsw_batch {
   gbbsw::Pair *d_pairs = nullptr;
   uint8_t *d_tgt = nullptr, *d_qry = nullptr;
   int32_t *d_out6 = nullptr, *d_cells = nullptr;
-  unsigned long long *d_total = nullptr;  // [0] total cells, [1] wave-kernel work counter, [2..6] segment kernels
-  static constexpr int kTotals = 8;
+  unsigned long long *d_total = nullptr;  // [0] total cells, [1] work counter
+  static constexpr int kTotals = 2;
   size_t cap_n = 0, cap_tgt = 0, cap_qry = 0;  // allocated capacities (cached workspaces are refilled)
   bool ran = false;
 };
@@ -989,9 +764,6 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
   // 0.28 us: ~1.4 ms for 250 rows at NCH 20), while the wave-per-pair kernel takes such a pair in
   // tens of microseconds. The fraction GB_BSW_TAIL (default 0.1) of the lane pairs with the
   // largest rows x chunks moves to the wave-per-pair kernel, which runs beside the lane kernels.
-  // GB_BSW_SEG (fraction, default 0) routes the next-largest lane pairs to the segment-per-pair kernel
-  // (16 lanes per pair, variants 6..10 by query length): a row of a long pair then takes a 16th of a
-  // pair-per-lane lane's time. Both cuts rank the lane pairs by rows x chunks.
   {
     const char *te = getenv("GB_BSW_TAIL");
     // r03ab, 100 k pairs: 0 228, 0.05 234, 0.1 258, 0.2 243 GCUPS. A batch of fewer lane waves than
@@ -999,37 +771,21 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     // critical path long: every lane pair goes to the wave-per-pair kernel (1.30 -> 0.56 ms,
     // profiles/r05b_bsw_small.log)
     const double frac = te ? atof(te) : (n < (int64_t)64 * 4 * std::max(B->num_cus, 1) ? 1.0 : 0.1);
-    const char *se = getenv("GB_BSW_SEG");
-    const double sfrac = se ? atof(se) : 0.0;
     const int64_t fill = (int64_t)64 * 8 * std::max(B->num_cus, 1);  // lane waves of 64 pairs, 2 per SIMD
-    if ((frac > 0 || sfrac > 0) && (n >= 1024 || frac >= 1.0) && n <= 2 * fill) {
-      auto cost_of = [&](int64_t p) { return (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)); };
+    if (frac > 0 && (n >= 1024 || frac >= 1.0) && n <= 2 * fill) {
       std::vector<uint32_t> cost;
       cost.reserve((size_t)n);
       for (int64_t p = 0; p < n; ++p)
-        if (var[p] < 5 && P[p].h0 != 0) cost.push_back(cost_of(p));
-      const size_t kt = (size_t)((double)cost.size() * std::min(1.0, frac));
-      const size_t ks = std::min(cost.size(), kt + (size_t)((double)cost.size() * std::min(1.0, sfrac)));
-      uint32_t cut_t = UINT32_MAX, cut_s = UINT32_MAX;
-      if (kt > 0 && kt <= cost.size()) {
-        std::nth_element(cost.begin(), cost.end() - (ptrdiff_t)kt, cost.end());
-        cut_t = *(cost.end() - (ptrdiff_t)kt);
-      }
-      if (ks > kt && ks <= cost.size()) {
-        std::nth_element(cost.begin(), cost.end() - (ptrdiff_t)ks, cost.end());
-        cut_s = *(cost.end() - (ptrdiff_t)ks);
-      }
-      for (int64_t p = 0; p < n; ++p) {
-        if (!(var[p] < 5 && P[p].h0 != 0)) continue;
-        const uint32_t c = cost_of(p);
-        if (c >= cut_t && kt > 0) {
-          var[p] = 5;
-        } else if (c >= cut_s) {
-          var[p] = (uint8_t)(6 + var[p]);
-        } else {
-          continue;
-        }
-        keys[p] = sort_key(var[p], P[p]);
+        if (var[p] < 5 && P[p].h0 != 0) cost.push_back((uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)));
+      const size_t k = std::min(cost.size(), (size_t)((double)cost.size() * std::min(1.0, frac)));
+      if (k > 0) {
+        std::nth_element(cost.begin(), cost.end() - (ptrdiff_t)k, cost.end());
+        const uint32_t cut = *(cost.end() - (ptrdiff_t)k);
+        for (int64_t p = 0; p < n; ++p)
+          if (var[p] < 5 && P[p].h0 != 0 && (uint32_t)P[p].tlen * (uint32_t)(4 * (var[p] + 1)) >= cut) {
+            var[p] = 5;
+            keys[p] = sort_key(5, P[p]);
+          }
       }
     }
   }
@@ -1195,34 +951,6 @@ int gb_bsw_batch_run(gb_bsw_batch *B) {
       const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cap, (nw + gbbsw::kWavesPerBlock - 1) / gbbsw::kWavesPerBlock));
       hipLaunchKernelGGL(gbbsw::bsw_extend_kernel, dim3((unsigned)blocks), dim3(64 * gbbsw::kWavesPerBlock), 0,
                          B->side[5], A);
-      GB_HIP(hipGetLastError());
-    }
-    void (*seg_kernels[5])(gbbsw::SegArgs) = {gbbsw::bsw_seg_kernel<2>, gbbsw::bsw_seg_kernel<4>,
-                                              gbbsw::bsw_seg_kernel<6>, gbbsw::bsw_seg_kernel<8>,
-                                              gbbsw::bsw_seg_kernel<10>};
-    for (int v = 6; v < gb_bsw_batch::kVariants; ++v) {
-      const int64_t cnt = B->seg[v + 1] - B->seg[v];
-      if (cnt == 0) continue;
-      gbbsw::SegArgs S;
-      S.pairs = B->d_pairs;
-      S.list = B->d_order + B->seg[v];
-      S.count = cnt;
-      S.tgt = B->d_tgt;
-      S.qry = B->d_qry;
-      S.out6 = B->d_out6;
-      S.cells = B->d_cells;
-      S.total_cells = B->d_total;
-      S.next = reinterpret_cast<unsigned int *>(B->d_total + 2 + (v - 6));
-      S.o_del = B->params.o_del;
-      S.e_del = B->params.e_del;
-      S.o_ins = B->params.o_ins;
-      S.e_ins = B->params.e_ins;
-      S.zdrop = B->params.zdrop;
-      for (int t = 0; t < 10; ++t) S.tab[t] = L.tab[t];
-      // persistent: at most 32 waves per CU, groups of four pairs handed out by the counter
-      const int64_t groups = (cnt + 3) / 4;
-      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)B->num_cus * 32));
-      hipLaunchKernelGGL(seg_kernels[v - 6], dim3((unsigned)blocks), dim3(64), 0, B->side[v], S);
       GB_HIP(hipGetLastError());
     }
   }

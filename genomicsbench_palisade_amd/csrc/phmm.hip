@@ -944,6 +944,40 @@ struct HostClock {
   }
 };
 
+// Device buffers of a batch for n testcases and a pool of pool_bytes (grow-only). The pipelined path
+// reserves every chunk's buffers before its first launch: an allocation that grows a buffer frees
+// the old one, and hipFree waits for the device.
+int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
+  const size_t nn = std::max(n, 1);
+  if (nn > b->cap_n) {
+    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
+                    (void *)b->d_stacks})
+      (void)hipFree(p);
+    b->d_desc = nullptr;
+    b->d_rf = nullptr;
+    b->d_rd = b->d_out = nullptr;
+    b->d_stk_tc = nullptr;
+    b->d_stacks = nullptr;
+    b->cap_n = 0;
+    GB_HIP(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
+    GB_HIP(hipMalloc(&b->d_rf, sizeof(float) * nn));
+    GB_HIP(hipMalloc(&b->d_rd, sizeof(double) * nn));
+    GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
+    GB_HIP(hipMalloc(&b->d_stk_tc, sizeof(uint32_t) * nn));
+    GB_HIP(hipMalloc(&b->d_stacks, sizeof(Stack) * nn));  // at most one stack per testcase
+    b->cap_n = nn;
+  }
+  if (pool_bytes > b->cap_pool) {
+    (void)hipFree(b->d_pool);
+    b->d_pool = nullptr;
+    b->cap_pool = 0;
+    GB_HIP(hipMalloc(&b->d_pool, pool_bytes));
+    b->cap_pool = pool_bytes;
+  }
+  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 4 * sizeof(int)));
+  return GB_OK;
+}
+
 int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   HostClock clk;
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
@@ -1168,33 +1202,7 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   pool.resize((pool.size() + 15) & ~size_t(15));
 
   clk.mark("stacks");
-  const size_t nn = std::max(n, 1);
-  if (nn > b->cap_n) {
-    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
-                    (void *)b->d_stacks})
-      (void)hipFree(p);
-    b->d_desc = nullptr;
-    b->d_rf = nullptr;
-    b->d_rd = b->d_out = nullptr;
-    b->d_stk_tc = nullptr;
-    b->d_stacks = nullptr;
-    b->cap_n = 0;
-    GB_HIP(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
-    GB_HIP(hipMalloc(&b->d_rf, sizeof(float) * nn));
-    GB_HIP(hipMalloc(&b->d_rd, sizeof(double) * nn));
-    GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
-    GB_HIP(hipMalloc(&b->d_stk_tc, sizeof(uint32_t) * nn));
-    GB_HIP(hipMalloc(&b->d_stacks, sizeof(Stack) * nn));  // at most one stack per testcase
-    b->cap_n = nn;
-  }
-  if (pool.size() > b->cap_pool) {
-    (void)hipFree(b->d_pool);
-    b->d_pool = nullptr;
-    b->cap_pool = 0;
-    GB_HIP(hipMalloc(&b->d_pool, pool.size()));
-    b->cap_pool = pool.size();
-  }
-  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 4 * sizeof(int)));
+  if (int st = batch_reserve(b, n, pool.size())) return st;
   if (n_long) {
     // records + codes of one long stack per workgroup of the persistent kLong grid
     b->long_grid = std::min(n_long, b->f64_grid);
@@ -1285,6 +1293,13 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     if (!B[c]) return st;
     B[c]->force_f64 = false;
   }
+  // every chunk's device buffers first (the pool at its undeduplicated size, an upper bound), so no
+  // allocation runs while an earlier chunk computes
+  for (int c = 0; c < k; c++) {
+    size_t pool_bytes = 16;
+    for (int t = lo[c]; t < lo[c + 1]; t++) pool_bytes += 5 * (size_t)std::max(tcs[t].rslen, 0) + std::max(tcs[t].haplen, 0);
+    if ((st = batch_reserve(B[c], lo[c + 1] - lo[c], (pool_bytes + 15) & ~(size_t)15))) return st;
+  }
   HostClock clk;
   auto fetch = [&](int c) {
     const int o = lo[c];
@@ -1293,11 +1308,13 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
   };
   for (int c = 0; c < k; c++) {
     if ((st = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c]))) return st;
+    clk.mark("chunk filled");
     if ((st = gb_phmm_batch_run(B[c]))) return st;
     if (c > 0 && (st = fetch(c - 1))) return st;
+    if (c > 0) clk.mark("previous chunk fetched");
   }
   st = fetch(k - 1);
-  clk.mark("pipelined compute");
+  clk.mark("last chunk fetched");
   return st;
 }
 

@@ -98,6 +98,12 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
         tcs.push_back(t);
       }
   std::vector<double> res(tcs.size());
+  if (getenv("GB_PHMM_HOSTPROF")) {
+    struct timeval tb;
+    gettimeofday(&tb, nullptr);
+    fprintf(stderr, "[phmm host] testcase construction %.3f ms\n",
+            1e3 * ((tb.tv_sec - t0.tv_sec) + 1e-6 * (tb.tv_usec - t0.tv_usec)));
+  }
   if (loops == 1) {
     // one pass: gb_phmm_compute pipelines big jobs (packing chunk c + 1 while chunk c computes)
     st = gb_phmm_compute(tcs.data(), (int)tcs.size(), res.data(), nullptr, nullptr, nullptr);

@@ -322,22 +322,3 @@ def test_gpu_dropin_512_pair_batches_from_threads():
                               p.qry.ctypes.data, 512, 8, got.ctypes.data)
     assert t > 0
     assert_same(got, oracle_lib.bsw_oracle(p, P, nthreads=8)[0], "512-pair batches")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("tail,seg", [("0", "1"), ("0.1", "0.5"), ("0", "0.3")])
-def test_gpu_segment_kernel_vs_oracle(golden, monkeypatch, tail, seg):
-    """The segment-per-pair kernel (16 lanes per pair; GB_BSW_SEG routes the longest lane pairs to it)
-    under every parameter set of the golden file, on the golden pairs and on random sets with long
-    targets, bit-exact against the oracle (cell counts included)."""
-    monkeypatch.setenv("GB_BSW_TAIL", tail)
-    monkeypatch.setenv("GB_BSW_SEG", seg)
-    gp, sets = golden
-    cases = [("golden", gp)] + [(f"seed {sd}", gen.bsw_pairs(n, seed=sd, qlen=ql, extra=ex))
-                                for sd, n, ql, ex in [(5, 20000, (10, 150), (0, 100)), (6, 4000, (1, 159), (0, 600))]]
-    for cname, p in cases:
-        for name, (P, _) in sets.items():
-            got, cells, tot = _gpu(p, P)
-            exp, ocells, otot = oracle_lib.bsw_oracle(p, P, nthreads=8)
-            assert_same(got, exp, f"{cname} {name} tail {tail} seg {seg}")
-            assert (cells == ocells).all() and tot == otot

@@ -17,7 +17,7 @@ if os.environ.get("BSW_LIB"):  # another build of libgb.so, to time two builds o
 from genomicsbench_palisade_amd import bsw, gen, set_device, shard  # noqa: E402
 
 KNOBS = ("GB_BSW_REFILL", "GB_BSW_PROF", "GB_BSW_SMALL", "GB_BSW_H0STEP", "GB_BSW_QSHIFT", "GB_BSW_KEYORD",
-         "GB_BSW_TAIL", "GB_BSW_SEG")
+         "GB_BSW_TAIL")
 set_device(0)
 # BSW_PAIRS: the set size (default the 'large' set; gen.BSW_SMALL_PAIRS for 'small')
 pairs = gen.bsw_dataset(int(os.environ["BSW_PAIRS"]), seed=11, threads=16) if os.environ.get("BSW_PAIRS") \
