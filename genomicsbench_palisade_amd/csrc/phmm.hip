@@ -371,7 +371,8 @@ __device__ __forceinline__ int scan_add(int v) {  // wave-wide inclusive prefix 
 template <typename T, bool kF64Pass>
 __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
                           const uint8_t *__restrict__ pool, const DevTab<T> &tab, T *__restrict__ raw_out,
-                          const float *__restrict__ raw_f, bool force, uint8_t *smem_raw) {
+                          const float *__restrict__ raw_f, bool force, uint8_t *smem_raw, int part = 0,
+                          int parts = 1) {
   const int lane = threadIdx.x;
   const int C = (int)S.C;
   // LDS: boundary records for columns [-kRecPad, C+kBndPad) and the haplotype codes for columns
@@ -382,7 +383,10 @@ __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__rest
 
   // the stack's testcases, compacted to those computed in this pass
   TcDesc d = {0, 0, 0, 0};
+  // the f64 pass may take a stack in `parts` work units: unit `part` takes the stack's entries
+  // [part * count / parts, (part + 1) * count / parts)
   bool act = lane < (int)S.count;
+  if (parts > 1) act = act && lane >= part * (int)S.count / parts && lane < (part + 1) * (int)S.count / parts;
   if (act) {
     d = descs[stk_tc[S.first + lane]];
     if constexpr (kF64Pass) act = force || raw_f[d.out_idx] < 1e-28f;  // MIN_ACCEPTED, pairhmm_common.h:16
@@ -760,12 +764,16 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
   if constexpr (kF64Pass || kLong) {
     int done = 0;
     int *next = counter + (kLong ? (kF64Pass ? 3 : 2) : 1);
+    // f64 pass over the LDS stacks: `parts` work units per stack (the top byte of `force`), so a job
+    // of few stacks per worker balances its fallback work finer
+    const int parts = (kF64Pass && !kLong) ? max(1, (force >> 8) & 0xFF) : 1;
     while (true) {
       int k = 0;
       if (threadIdx.x == 0) k = atomicAdd(next, 1);
       k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-      if (k >= nstacks) break;
-      done += phmm_stack<T, kF64Pass>(stacks[k], stk_tc, descs, pool, tab, raw_out, raw_f, force != 0, rec);
+      if (k >= nstacks * parts) break;
+      done += phmm_stack<T, kF64Pass>(stacks[k / parts], stk_tc, descs, pool, tab, raw_out, raw_f, (force & 0xFF) != 0,
+                                      rec, k % parts, parts);
       __syncthreads();  // the next stack re-initialises the records
     }
     if (kF64Pass && threadIdx.x == 0 && done) atomicAdd(counter, done);
@@ -895,6 +903,7 @@ struct gb_phmm_batch {
   int n = 0;
   int max_haplen = 0;
   int64_t cells = 0;
+  void *d_arena = nullptr;  // holds d_desc, d_rf, d_rd, d_out, d_stk_tc, d_stacks
   TcDesc *d_desc = nullptr;
   uint8_t *d_pool = nullptr;
   float *d_rf = nullptr;
@@ -916,6 +925,7 @@ struct gb_phmm_batch {
   bool force_f64 = false;
   int rpl = 1;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=2: two, for A/B probes)
   int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
+  int f64_parts = 1;  // work units per stack in the f64 pass (GB_PHMM_F64_PARTS)
 };
 
 extern "C" {
@@ -950,21 +960,32 @@ struct HostClock {
 int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
   const size_t nn = std::max(n, 1);
   if (nn > b->cap_n) {
-    for (void *p : {(void *)b->d_desc, (void *)b->d_rf, (void *)b->d_rd, (void *)b->d_out, (void *)b->d_stk_tc,
-                    (void *)b->d_stacks})
-      (void)hipFree(p);
+    // the six per-testcase arrays carved from one allocation (a cold process pays per hipMalloc)
+    (void)hipFree(b->d_arena);
+    b->d_arena = nullptr;
     b->d_desc = nullptr;
     b->d_rf = nullptr;
     b->d_rd = b->d_out = nullptr;
     b->d_stk_tc = nullptr;
     b->d_stacks = nullptr;
     b->cap_n = 0;
-    GB_HIP(hipMalloc(&b->d_desc, sizeof(TcDesc) * nn));
-    GB_HIP(hipMalloc(&b->d_rf, sizeof(float) * nn));
-    GB_HIP(hipMalloc(&b->d_rd, sizeof(double) * nn));
-    GB_HIP(hipMalloc(&b->d_out, sizeof(double) * nn));
-    GB_HIP(hipMalloc(&b->d_stk_tc, sizeof(uint32_t) * nn));
-    GB_HIP(hipMalloc(&b->d_stacks, sizeof(Stack) * nn));  // at most one stack per testcase
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t sz[6] = {up(sizeof(TcDesc) * nn), up(sizeof(float) * nn), up(sizeof(double) * nn),
+                          up(sizeof(double) * nn), up(sizeof(uint32_t) * nn),
+                          up(sizeof(Stack) * nn)};  // at most one stack per testcase
+    GB_HIP(hipMalloc(&b->d_arena, sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5]));
+    uint8_t *a = (uint8_t *)b->d_arena;
+    b->d_desc = (TcDesc *)a;
+    a += sz[0];
+    b->d_rf = (float *)a;
+    a += sz[1];
+    b->d_rd = (double *)a;
+    a += sz[2];
+    b->d_out = (double *)a;
+    a += sz[3];
+    b->d_stk_tc = (uint32_t *)a;
+    a += sz[4];
+    b->d_stacks = (Stack *)a;
     b->cap_n = nn;
   }
   if (pool_bytes > b->cap_pool) {
@@ -1157,6 +1178,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 2 ? 2 : 1;
   b->w2 = 0;
   if (const char *e = getenv("GB_PHMM_W2")) b->w2 = atoi(e);
+  b->f64_parts = 1;
+  if (const char *e = getenv("GB_PHMM_F64_PARTS")) b->f64_parts = std::max(1, std::min(8, atoi(e)));
   int stack_rows = kStackRows;
   while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
@@ -1377,10 +1400,10 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
     // f64 fallback: persistent grid over the stacks, each recomputing its flagged testcases
     if (ns > 0) {
-      const int g64 = std::min(ns, b->f64_grid);
+      const int g64 = std::min(ns * b->f64_parts, b->f64_grid);
       hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
                          b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
-                         b->d_count, b->force_f64 ? 1 : 0, (uint8_t *)nullptr, (size_t)0);
+                         b->d_count, (b->force_f64 ? 1 : 0) | (b->f64_parts << 8), (uint8_t *)nullptr, (size_t)0);
     }
     if (nl > 0)
       hipLaunchKernelGGL((phmm_forward<double, true, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
@@ -1477,13 +1500,8 @@ int gb_phmm_batch_stats(gb_phmm_batch *b, int64_t *testcases, int64_t *cells, in
 int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   if (!b) return GB_OK;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
-  (void)hipFree(b->d_desc);
+  (void)hipFree(b->d_arena);
   (void)hipFree(b->d_pool);
-  (void)hipFree(b->d_rf);
-  (void)hipFree(b->d_rd);
-  (void)hipFree(b->d_out);
-  (void)hipFree(b->d_stk_tc);
-  (void)hipFree(b->d_stacks);
   (void)hipFree(b->d_count);
   (void)hipFree(b->d_scratch);
   for (auto e : b->ev)

@@ -82,21 +82,36 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
   if (st) die("gb_phmm_init", st);
   struct timeval t0, t1;
   gettimeofday(&t0, nullptr);
-  std::vector<gb_testcase> tcs;
-  for (Batch *b : shard)
-    for (auto &r : b->reads)
-      for (auto &h : b->haps) {
-        gb_testcase t;
-        t.rslen = (int)r.bases.size();
-        t.haplen = (int)h.size();
-        t.hap = h.c_str();
-        t.rs = r.bases.c_str();
-        t.q = r.q.c_str();
-        t.i = r.i.c_str();
-        t.d = r.d.c_str();
-        t.c = r.c.c_str();
-        tcs.push_back(t);
-      }
+  // testcase construction (the reference's r-major loop, PairHMMUnitTest.cpp:564-579), batches
+  // spread over a few host threads at precomputed offsets
+  std::vector<size_t> off(shard.size() + 1, 0);
+  for (size_t k = 0; k < shard.size(); k++) off[k + 1] = off[k] + shard[k]->reads.size() * shard[k]->haps.size();
+  std::vector<gb_testcase> tcs(off.back());
+  auto build = [&](size_t k0, size_t k1) {
+    for (size_t k = k0; k < k1; k++) {
+      gb_testcase *t = tcs.data() + off[k];
+      for (auto &r : shard[k]->reads)
+        for (auto &h : shard[k]->haps) {
+          t->rslen = (int)r.bases.size();
+          t->haplen = (int)h.size();
+          t->hap = h.c_str();
+          t->rs = r.bases.c_str();
+          t->q = r.q.c_str();
+          t->i = r.i.c_str();
+          t->d = r.d.c_str();
+          t->c = r.c.c_str();
+          ++t;
+        }
+    }
+  };
+  const size_t nth = std::min<size_t>(8, std::max<size_t>(1, shard.size() / 4));
+  if (nth == 1) {
+    build(0, shard.size());
+  } else {
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nth; t++) th.emplace_back(build, shard.size() * t / nth, shard.size() * (t + 1) / nth);
+    for (auto &x : th) x.join();
+  }
   std::vector<double> res(tcs.size());
   if (getenv("GB_PHMM_HOSTPROF")) {
     struct timeval tb;
