@@ -553,8 +553,7 @@ int launch_table(gb_chain_batch *B, int prof) {
     // chain_rows blocks on the batch stream (their targets / scratch marks cleared first), the
     // rest (unsorted calls: rare) on the second stream beside them
     const int nr = B->n_rows, nvc = (int)B->vc.size(), ns = B->n_small;
-    GB_HIP(hipMemsetAsync(B->d_out + 2 * std::max<int64_t>(B->nanchors, 1), 0, (size_t)B->nanchors * 4, B->stream));
-    if (B->scratch_n > 0) GB_HIP(hipMemsetAsync(B->d_smark, 0, (size_t)B->scratch_n * 4, B->stream));
+    // (the targets output and the scratch marks were cleared by step_clear)
     if (nr < nvc) {
       GB_HIP(hipEventRecord(B->fj[0], B->stream));
       GB_HIP(hipStreamWaitEvent(B->stream2, B->fj[0], 0));
@@ -627,8 +626,12 @@ int gb_chain_batch_run(gb_chain_batch *B) {
   gb::Range range_("gb.chain.batch_run");
   GB_ARG(B, "gb_chain_batch_run: null batch");
   GB_HIP(hipSetDevice(B->device));
-  GB_HIP(hipMemsetAsync(B->d_vis, 0, sizeof(unsigned long long), B->stream));
   GB_HIP(hipEventRecord(B->ev[0], B->stream));
+  if (B->n_rows > 0 || !B->split.empty()) {
+    if (int st = gbchain::step_clear_launch(B)) return st;
+  } else {
+    GB_HIP(hipMemsetAsync(B->d_vis, 0, sizeof(unsigned long long), B->stream));
+  }
   if (B->ncalls > 0) {
     const char *pe = getenv("GB_CHAIN_PROF");
     const int prof = (pe && (*pe == '1' || *pe == '2')) ? *pe - '0' : 0;

@@ -99,6 +99,7 @@ namespace gbchain {
 // chain_split.hip
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4);
 int split_resolve(gb_chain_batch *B);
+int step_clear_launch(gb_chain_batch *B);  // every per-step clear in one launch (before the blocks)
 void split_free(gb_chain_batch *B);
 int launch_chain(gb_chain_batch *B, const VCall *d_vc, int nvc, int prof, bool small, hipStream_t stream);
 int launch_table(gb_chain_batch *B, int prof);

@@ -116,6 +116,30 @@ __global__ __launch_bounds__(64) void guess_init(SplitArgs A, int32_t *link, int
   val[j] = v;
 }
 
+// The clears of one step in one launch (each hipMemset is a dispatch of its own, ~5 us at the launch
+// floor, and a step had eight of them): the targets output and chain_rows' scratch marks before the
+// blocks run, and the split resolution's first-round state -- t2 marks, per-call visited counts,
+// failure flags, verify_kernel's work-list count, front = c1 (was a host copy per step).
+__global__ __launch_bounds__(256) void step_clear(SplitArgs A, int32_t *targets, int64_t nanchors, int32_t *smark,
+                                                  int64_t scratch_n, unsigned long long *vis, int32_t ns,
+                                                  int32_t *front) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = t; i < nanchors; i += stride) {
+    targets[i] = 0;
+    if (ns > 0) A.t2[i] = 0;
+  }
+  for (int64_t i = t; i < scratch_n; i += stride) smark[i] = 0;
+  for (int64_t k = t; k < ns; k += stride) {
+    front[k] = A.split[k].c1;
+    A.fail[k] = 0x7f7f7f7f;
+    A.viscall[k] = 0;
+  }
+  if (t == 0) {
+    *vis = 0;
+    if (ns > 0) A.slow[0] = 0;
+  }
+}
+
 // one pointer-jumping round: OP 0 adds (guesses), OP 1 takes the maximum (peaks)
 template <int OP>
 __global__ __launch_bounds__(256) void jump_round(int64_t n, const int32_t *li, const int32_t *vi, int32_t *lo,
@@ -790,6 +814,17 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   return GB_OK;
 }
 
+int step_clear_launch(gb_chain_batch *B) {
+  const int64_t ns = (int64_t)B->split.size();
+  const SplitArgs A = ns ? split_args(B) : SplitArgs{};
+  const int64_t work = std::max<int64_t>(std::max<int64_t>(B->nanchors, B->scratch_n), ns);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 4096));
+  hipLaunchKernelGGL(step_clear, dim3(g), dim3(256), 0, B->stream, A, B->d_out + 2 * std::max<int64_t>(B->nanchors, 1),
+                     B->nanchors, B->d_smark, B->scratch_n, B->d_vis, (int32_t)ns, B->d_front);
+  GB_HIP(hipGetLastError());
+  return GB_OK;
+}
+
 int split_resolve(gb_chain_batch *B) {
   gb::Range range_("gb.chain.split_resolve");
   const int64_t ns = (int64_t)B->split.size();
@@ -803,10 +838,8 @@ int split_resolve(gb_chain_batch *B) {
     B->cap_hfail = ns;
   }
   const int32_t *fail = B->h_fail;
+  // front = c1, t2, viscall, fail and the work-list count were cleared by step_clear at the step's start
   for (int64_t k = 0; k < ns; k++) front[(size_t)k] = B->split[(size_t)k].c1;
-  GB_HIP(hipMemcpyAsync(B->d_front, front.data(), (size_t)ns * 4, hipMemcpyHostToDevice, B->stream));
-  GB_HIP(hipMemsetAsync(B->d_t2, 0, (size_t)B->nanchors * 4, B->stream));
-  GB_HIP(hipMemsetAsync(B->d_viscall, 0, (size_t)ns * 8, B->stream));
   const SplitArgs A = split_args(B);
   // global rounds after jump_local: hops between tiles
   const int rounds = jump_rounds(B->max_split_n / kTile + 2);
@@ -834,9 +867,9 @@ int split_resolve(gb_chain_batch *B) {
     hipLaunchKernelGGL(guess_init, dim3(nch), dim3(64), 0, B->stream, A, B->d_link[0], B->d_val[0]);
     const int r = jump(B, 0, rounds);
     hipLaunchKernelGGL(guess_write, dim3(nch), dim3(64), 0, B->stream, A, (const int32_t *)B->d_val[r]);
-    GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
+    if (B->spec_rounds > 1) GB_HIP(hipMemsetAsync(B->d_fail, 0x7f, (size_t)ns * 4, B->stream));
     if (lanes) {
-      GB_HIP(hipMemsetAsync(B->d_slow, 0, sizeof(int32_t), B->stream));
+      if (B->spec_rounds > 1) GB_HIP(hipMemsetAsync(B->d_slow, 0, sizeof(int32_t), B->stream));
       hipLaunchKernelGGL(verify_lanes<true>, dim3(nch), dim3(64), 0, B->stream, A, B->d_need);
       hipLaunchKernelGGL(verify_kernel<true>, dim3(slow_grid), dim3(64), 0, B->stream, A, (const uint64_t *)B->d_need);
     } else {
