@@ -1325,8 +1325,16 @@ int warm_up(DeviceTables *t) {
                      b->d_out, 0, t->hf.log10_init, t->hd.log10_init);
   GB_HIP(hipGetLastError());
   GB_HIP(hipStreamSynchronize(b->stream));
-  for (int c = 1; c < kPipeMaxChunks; c++)
-    if (!thread_workspace(t, &st, c)) return st;
+  // the runtime creates a stream's hardware queue at its first command (~10-15 ms, measured inside
+  // bin/phmm's timed region as a chunk upload): give each workspace stream one here
+  for (int c = 1; c < kPipeMaxChunks; c++) {
+    gb_phmm_batch *w = thread_workspace(t, &st, c);
+    if (!w) return st;
+    if ((st = batch_reserve(w, 1, 16))) return st;
+    GB_HIP(hipMemsetAsync(w->d_count, 0, 4 * sizeof(int), w->stream));
+    GB_HIP(hipEventRecord(w->ev[0], w->stream));
+  }
+  for (int c = 1; c < kPipeMaxChunks; c++) GB_HIP(hipStreamSynchronize(thread_workspace(t, &st, c)->stream));
   return GB_OK;
 }
 
