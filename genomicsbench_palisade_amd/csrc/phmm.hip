@@ -778,9 +778,13 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
     }
     if (kF64Pass && threadIdx.x == 0 && done) atomicAdd(counter, done);
   } else {
-    if ((int)blockIdx.x < nstacks)  // gb_phmm_init's warm-up launch has no stacks
-      phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec);
+    phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec);
   }
+}
+
+// gb_phmm_init's warm-up launch (no work)
+__global__ void phmm_warm(int *count) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) count[3] = 0;
 }
 
 // Device log10 epilogue (IntelPairHmmCSource.cpp:73-79); the host path recomputes it bit-exactly.
@@ -1314,15 +1318,9 @@ int warm_up(DeviceTables *t) {
   gb_phmm_batch *b = thread_workspace(t, &st, 0);
   if (!b) return st;
   if ((st = batch_reserve(b, 1, 16))) return st;
-  GB_HIP(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), b->stream));
-  hipLaunchKernelGGL((phmm_forward<float, false>), dim3(1), dim3(kWave), 0, b->stream, b->d_stacks, 0, b->d_stk_tc,
-                     b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
-                     b->d_count, 0, (uint8_t *)nullptr, (size_t)0);
-  hipLaunchKernelGGL((phmm_forward<double, true>), dim3(1), dim3(kWave), 0, b->stream, b->d_stacks, 0, b->d_stk_tc,
-                     b->d_desc, b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
-                     b->d_count, 1 << 8, (uint8_t *)nullptr, (size_t)0);
-  hipLaunchKernelGGL(phmm_finalize, dim3(1), dim3(256), 0, b->stream, b->d_rf, b->d_rd, (const uint8_t *)nullptr,
-                     b->d_out, 0, t->hf.log10_init, t->hd.log10_init);
+  // one launch of a no-op kernel of this module loads the module's code object (every phmm kernel);
+  // a no-op of its own keeps the profiles' per-kernel statistics free of empty dispatches
+  hipLaunchKernelGGL(phmm_warm, dim3(1), dim3(kWave), 0, b->stream, b->d_count);
   GB_HIP(hipGetLastError());
   GB_HIP(hipStreamSynchronize(b->stream));
   // the runtime creates a stream's hardware queue at its first command (~10-15 ms, measured inside
