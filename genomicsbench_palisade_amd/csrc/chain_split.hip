@@ -633,6 +633,9 @@ int jump(gb_chain_batch *B, int op, int rounds) {
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4) {
   int seg, warm, trunc, wcap;
   split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm, &trunc, &wcap);
+  // GB_CHAIN_TARGET: the longest block in rows a split tries to stay under (0: equal segments of seg)
+  const char *te = getenv("GB_CHAIN_TARGET");
+  const int32_t target = te ? std::max(0, atoi(te)) : 0;
   const int64_t ncalls = B->ncalls;
   B->vc.clear();
   B->split.clear();
@@ -682,7 +685,9 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
       th.emplace_back([&, t] {
         for (int64_t c = t; c < ncalls; c += nt) {
           const int32_t n = (int32_t)(offsets[c + 1] - offsets[c]);
-          if (seg < 64 || (int64_t)n < 2 * (int64_t)seg) {
+          const bool maybe = seg >= 64 && (target > 0 ? (int64_t)n > std::min<int64_t>(target, 2 * (int64_t)seg)
+                                                      : (int64_t)n >= 2 * (int64_t)seg);
+          if (!maybe) {
             walk(c, nullptr);
             continue;
           }
@@ -693,9 +698,21 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
             K.st = std::vector<int32_t>();
             continue;
           }
-          // equal segments of at most seg anchors: the longest block of the launch (a segment, its
-          // window and its warm-up) is then bounded by seg, not by a last segment of up to 2 seg - 1
-          const int32_t nseg = (n + seg - 1) / seg, L = (n + nseg - 1) / nseg;
+          // with a row target: a call's segments are as long as its window leaves room for under the
+          // target (block = warm-up + capped window + segment), and a call no longer than the target
+          // runs whole
+          int32_t segc = seg;
+          if (target > 0) {
+            if (n <= target) {
+              K.st = std::vector<int32_t>();
+              continue;
+            }
+            const int32_t cw = std::min(maxwin[(size_t)c], wcap);
+            segc = std::max(128, std::min(seg, target - cw - warm));
+          }
+          // equal segments of at most segc anchors: the longest block of the launch (a segment, its
+          // window and its warm-up) is then bounded by segc, not by a last segment of up to 2 segc - 1
+          const int32_t nseg = (n + segc - 1) / segc, L = (n + nseg - 1) / nseg;
           K.L = L;
           K.as.resize((size_t)nseg);
           K.win.resize((size_t)nseg);

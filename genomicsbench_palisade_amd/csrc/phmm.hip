@@ -1368,15 +1368,21 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     return gb_phmm_batch_results(B[c], results ? results + o : nullptr, raw_f ? raw_f + o : nullptr,
                                  raw_d ? raw_d + o : nullptr, used_double ? used_double + o : nullptr, nullptr);
   };
+  // chunk c - 2's results are fetched after chunk c is launched: the host never waits on the chunk
+  // the GPU has just started, only on one queued behind it, and packs ahead meanwhile
+  int fetched = 0;
   for (int c = 0; c < k; c++) {
     if ((st = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c]))) return st;
     clk.mark("chunk filled");
     if ((st = gb_phmm_batch_run(B[c]))) return st;
-    if (c > 0 && (st = fetch(c - 1))) return st;
-    if (c > 0) clk.mark("previous chunk fetched");
+    if (c >= 2) {
+      if ((st = fetch(fetched++))) return st;
+      clk.mark("chunk fetched");
+    }
   }
-  st = fetch(k - 1);
-  clk.mark("last chunk fetched");
+  while (fetched < k)
+    if ((st = fetch(fetched++))) return st;
+  clk.mark("last chunks fetched");
   return st;
 }
 

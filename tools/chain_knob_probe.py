@@ -18,12 +18,14 @@ from genomicsbench_palisade_amd import chain, gen, set_device, shard  # noqa: E4
 
 set_device(0)
 large = gen.chain_dataset("large", seed=5)
-sets = [("shard0/8", shard.shard_calls(large, 0, 8)[0]), ("large", large)]
+small = gen.chain_dataset("small", seed=5)
+sets = [("shard0/8", shard.shard_calls(large, 0, 8)[0]), ("large", large),
+        ("s_shard0/8", shard.shard_calls(small, 0, 8)[0]), ("small", small)]
 if os.environ.get("CHAIN_SETS"):
     sets = [s for s in sets if s[0] in os.environ["CHAIN_SETS"].split(",")]
 configs = os.environ.get("CHAIN_CONFIGS", "").split(";")
 KNOBS = ("GB_CHAIN_SPLIT", "GB_CHAIN_ROWS", "GB_CHAIN_ROWS_MAXN", "GB_CHAIN_VLANES", "GB_CHAIN_PRIO", "GB_CHAIN_SPREAD",
-         "GB_CHAIN_EXP")
+         "GB_CHAIN_EXP", "GB_CHAIN_TARGET")
 
 
 def parse_cfg(cfg):
