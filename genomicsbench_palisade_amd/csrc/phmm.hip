@@ -908,6 +908,8 @@ struct gb_phmm_batch {
   int n = 0;
   int max_haplen = 0;
   int64_t cells = 0;
+  uint8_t *h_stage = nullptr;  // pinned upload staging (grow-only)
+  size_t cap_stage = 0;
   void *d_arena = nullptr;  // holds d_desc, d_rf, d_rd, d_out, d_stk_tc, d_stacks
   TcDesc *d_desc = nullptr;
   uint8_t *d_pool = nullptr;
@@ -1007,6 +1009,17 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
     b->cap_pool = pool_bytes;
   }
   if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 4 * sizeof(int)));
+  return GB_OK;
+}
+
+// grow-only pinned staging buffer of a batch (uploads)
+int stage_reserve(gb_phmm_batch *b, size_t bytes) {
+  if (bytes <= b->cap_stage) return GB_OK;
+  if (b->h_stage) (void)hipHostFree(b->h_stage);
+  b->h_stage = nullptr;
+  b->cap_stage = 0;
+  GB_HIP(hipHostMalloc((void **)&b->h_stage, bytes, hipHostMallocDefault));
+  b->cap_stage = bytes;
   return GB_OK;
 }
 
@@ -1253,14 +1266,28 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       b->cap_scratch = need;
     }
   }
-  if (n) {
-    GB_HIP(hipMemcpyAsync(b->d_desc, desc.data(), sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
-    GB_HIP(hipMemcpyAsync(b->d_stk_tc, stk_tc.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
-    GB_HIP(hipMemcpyAsync(b->d_stacks, sorted_stacks.data(), sizeof(Stack) * sorted_stacks.size(),
-                          hipMemcpyHostToDevice, b->stream));
+  // the uploads go through the batch's pinned staging buffer: a pageable copy is staged by the
+  // runtime, and while an earlier chunk's kernels held the GPU one chunk's upload waited 10-15 ms
+  // for it (profiles/r05j_phmm_cli.log); a pinned copy is a plain DMA
+  {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o1 = up(sizeof(TcDesc) * n), o2 = o1 + up(sizeof(uint32_t) * n),
+                 o3 = o2 + up(sizeof(Stack) * sorted_stacks.size()), tot = o3 + pool.size();
+    if (int st = stage_reserve(b, tot)) return st;
+    uint8_t *h = b->h_stage;
+    if (n) {
+      std::memcpy(h, desc.data(), sizeof(TcDesc) * n);
+      std::memcpy(h + o1, stk_tc.data(), sizeof(uint32_t) * n);
+      std::memcpy(h + o2, sorted_stacks.data(), sizeof(Stack) * sorted_stacks.size());
+      GB_HIP(hipMemcpyAsync(b->d_desc, h, sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
+      GB_HIP(hipMemcpyAsync(b->d_stk_tc, h + o1, sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
+      GB_HIP(hipMemcpyAsync(b->d_stacks, h + o2, sizeof(Stack) * sorted_stacks.size(), hipMemcpyHostToDevice,
+                            b->stream));
+    }
+    std::memcpy(h + o3, pool.data(), pool.size());
+    GB_HIP(hipMemcpyAsync(b->d_pool, h + o3, pool.size(), hipMemcpyHostToDevice, b->stream));
   }
-  GB_HIP(hipMemcpyAsync(b->d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice, b->stream));
-  GB_HIP(hipStreamSynchronize(b->stream));  // the host vectors die on return
+  GB_HIP(hipStreamSynchronize(b->stream));  // the staging buffer is reused by the next fill
   clk.mark("upload");
   b->n = n;
   b->nstacks = (int)sorted_stacks.size() - n_long;
@@ -1355,12 +1382,29 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     if (!B[c]) return st;
     B[c]->force_f64 = false;
   }
-  // every chunk's device buffers first (the pool at its undeduplicated size, an upper bound), so no
-  // allocation runs while an earlier chunk computes
+  // every chunk's per-testcase device arrays and a pinned staging buffer first, so few allocations
+  // run while an earlier chunk computes. The pool is estimated as the reads that change from one
+  // testcase to the next (the reference's r-major order) plus the haplotypes not seen lately;
+  // batch_fill grows both buffers should the packed pool be larger.
   for (int c = 0; c < k; c++) {
     size_t pool_bytes = 16;
-    for (int t = lo[c]; t < lo[c + 1]; t++) pool_bytes += 5 * (size_t)std::max(tcs[t].rslen, 0) + std::max(tcs[t].haplen, 0);
-    if ((st = batch_reserve(B[c], lo[c + 1] - lo[c], (pool_bytes + 15) & ~(size_t)15))) return st;
+    const char *prev_rs = nullptr;
+    const char *hseen[512] = {};  // direct-mapped: a collision only overestimates
+    for (int t = lo[c]; t < lo[c + 1]; t++) {
+      if (tcs[t].rs != prev_rs) {
+        pool_bytes += 5 * (size_t)std::max(tcs[t].rslen, 0);
+        prev_rs = tcs[t].rs;
+      }
+      const size_t hs = ((uintptr_t)tcs[t].hap >> 4) % 512;
+      if (hseen[hs] != tcs[t].hap) {
+        hseen[hs] = tcs[t].hap;
+        pool_bytes += (size_t)std::max(tcs[t].haplen, 0);
+      }
+    }
+    pool_bytes = (pool_bytes + pool_bytes / 4 + 15) & ~(size_t)15;
+    const int m = lo[c + 1] - lo[c];
+    if ((st = batch_reserve(B[c], m, pool_bytes))) return st;
+    if ((st = stage_reserve(B[c], 36 * (size_t)m + 1024 + pool_bytes))) return st;
   }
   HostClock clk;
   auto fetch = [&](int c) {
@@ -1547,6 +1591,7 @@ int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   (void)hipFree(b->d_arena);
   (void)hipFree(b->d_pool);
+  if (b->h_stage) (void)hipHostFree(b->h_stage);
   (void)hipFree(b->d_count);
   (void)hipFree(b->d_scratch);
   for (auto e : b->ev)
