@@ -633,9 +633,13 @@ int jump(gb_chain_batch *B, int op, int rounds) {
 int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, const int32_t *params4) {
   int seg, warm, trunc, wcap;
   split_knobs(B->ncalls ? offsets[B->ncalls] : 0, &seg, &warm, &trunc, &wcap);
-  // GB_CHAIN_TARGET: the longest block in rows a split tries to stay under (0: equal segments of seg)
+  // A row target: the longest block a split tries to stay under (0: equal segments of seg). A batch
+  // this small is its longest block: the 1/8 shard of the 'small' set (318 k anchors) 0.89 -> 0.68 ms
+  // at 600 rows; bigger batches have the work to lose (the 'large' 1/8 shard, 3.2 M anchors: 1.37 ->
+  // 1.42 ms at 900, 'large' 5.0 -> 8.9 ms; profiles/r05j_chain_target.log). GB_CHAIN_TARGET overrides.
+  const int64_t total = B->ncalls ? offsets[B->ncalls] : 0;
   const char *te = getenv("GB_CHAIN_TARGET");
-  const int32_t target = te ? std::max(0, atoi(te)) : 0;
+  const int32_t target = te ? std::max(0, atoi(te)) : (total < (1 << 20) ? 600 : 0);
   const int64_t ncalls = B->ncalls;
   B->vc.clear();
   B->split.clear();

@@ -253,3 +253,24 @@ def test_gpu_rows_long_windows(monkeypatch, split):
     assert_same(got, exp)
     assert got[4] == exp[4]
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("target", ["600", "300", "0"])
+def test_gpu_split_row_target(target, monkeypatch):
+    """Per-call segment lengths under a row target (GB_CHAIN_TARGET; a batch under 1 M anchors takes
+    600 by default): calls longer than the target split into segments as long as their window leaves
+    room for, shorter ones run whole -- bit-exact against the oracle either way."""
+    from genomicsbench_palisade_amd import chain, set_device
+    set_device(0)
+    monkeypatch.setenv("GB_CHAIN_TARGET", target)
+    calls = gen.chain_dataset("small", num_calls=300, seed=31, median_n=1500, max_n=30000)
+    exp = oracle_lib.chain_oracle(calls, 8)
+    b = chain.ChainBatch(calls)
+    b.run()
+    got = b.results()
+    assert_same(got, exp)
+    assert got[4] == exp[4]
+    if target != "0":
+        assert b.split_stats()[0] > 0
+    b.close()
