@@ -155,6 +155,8 @@ def test_gpu_split_exact(split_calls, monkeypatch, split, fault, rows):
     monkeypatch.setenv("GB_CHAIN_SPLIT", split)
     monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
     monkeypatch.setenv("GB_CHAIN_ROWS", rows)
+    # equal segments of `seg` (the per-call row target has test_gpu_split_row_target)
+    monkeypatch.setenv("GB_CHAIN_TARGET", "0")
     b = chain.ChainBatch(calls)
     b.run()
     got = b.results()
