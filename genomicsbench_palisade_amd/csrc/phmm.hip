@@ -29,7 +29,9 @@
 #include <chrono>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <mutex>
+#include <string>
 #include <unordered_map>
 #include <thread>
 #include <type_traits>
@@ -933,6 +935,11 @@ struct gb_phmm_batch {
   int rpl = 1;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=2: two, for A/B probes)
   int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
   int f64_parts = 2;  // work units per stack in the f64 pass (GB_PHMM_F64_PARTS)
+  // host scratch of the fills (grow-only, host_reserve)
+  std::vector<uint32_t> hid;
+  std::vector<Stack> stacks;
+  std::vector<uint64_t> skeys;
+  std::vector<std::vector<uint8_t>> pools;
 };
 
 namespace {
@@ -1012,25 +1019,63 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
   return GB_OK;
 }
 
-// grow-only pinned staging buffer of a batch (uploads)
-int stage_reserve(gb_phmm_batch *b, size_t bytes) {
+// grow-only pinned staging buffer of a batch (uploads, results); its first `keep` bytes survive a growth
+int stage_reserve(gb_phmm_batch *b, size_t bytes, size_t keep = 0) {
   if (bytes <= b->cap_stage) return GB_OK;
-  if (b->h_stage) (void)hipHostFree(b->h_stage);
-  b->h_stage = nullptr;
-  b->cap_stage = 0;
-  GB_HIP(hipHostMalloc((void **)&b->h_stage, bytes, hipHostMallocDefault));
+  uint8_t *h = nullptr;
+  GB_HIP(hipHostMalloc((void **)&h, bytes, hipHostMallocDefault));
+  if (b->h_stage) {
+    if (keep) std::memcpy(h, b->h_stage, std::min(keep, b->cap_stage));
+    (void)hipHostFree(b->h_stage);
+  }
+  b->h_stage = h;
   b->cap_stage = bytes;
   return GB_OK;
 }
 
-int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
+// Host scratch of a batch's fills for n testcases and pack pools of pool_bytes in all, kept across
+// fills and touched here: a fresh vector pays a page fault per 4 KiB at its first write, and several
+// fills faulting at once serialise on the process's memory map.
+void host_reserve(gb_phmm_batch *b, size_t n, size_t pool_bytes, int threads) {
+  if (b->hid.size() < n) b->hid.assign(n, 0);
+  if (b->stacks.size() < n) b->stacks.assign(n, Stack{});
+  if (b->skeys.size() < 2 * n) b->skeys.assign(2 * n, 0);
+  if ((int)b->pools.size() < threads) b->pools.resize(threads);
+  for (int t = 0; t < threads; t++) {
+    auto &P = b->pools[t];
+    const size_t want = pool_bytes / threads + 4096;
+    if (P.capacity() < want) {
+      P.clear();
+      P.shrink_to_fit();
+      P.resize(want);  // touch
+    }
+    P.clear();
+  }
+}
+
+// Staging layout of a fill of n testcases and a pool of pool_bytes: descriptors | stack testcase
+// lists | stacks (at most one per testcase) | pool
+struct StageLayout {
+  size_t o_tc, o_stk, o_pool, total;
+  StageLayout(size_t n, size_t pool_bytes) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    o_tc = up(sizeof(TcDesc) * n);
+    o_stk = o_tc + up(sizeof(uint32_t) * n);
+    o_pool = o_stk + up(sizeof(Stack) * n);
+    total = o_pool + up(pool_bytes) + 256;
+  }
+};
+
+// threads: host threads of the pack and merge phases (0: up to 8 for jobs of 64 K testcases and more)
+int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0) {
   HostClock clk;
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
   // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once. Inputs are validated
   // first (sequentially, so the error names the first bad testcase), then big jobs pack in
   // contiguous chunks on several threads, each with its own pool and maps; chunk pools are
   // concatenated and haplotype ids are made global in first-appearance order, which is the id order
-  // a single pass gives (a read shared across a chunk edge is stored once per chunk).
+  // a single pass gives (a read shared across a chunk edge is stored once per chunk). Descriptors,
+  // stack lists, stacks and pool are written straight into the pinned staging buffer.
   for (int k = 0; k < n; k++) {
     const gb_testcase &t = tcs[k];
     GB_ARG(t.rslen >= 1 && t.rslen <= 65535, "testcase %d: rslen %d outside [1,65535]", k, t.rslen);
@@ -1039,17 +1084,21 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
   }
   clk.mark("validate");
-  std::vector<TcDesc> desc(n);
-  std::vector<uint32_t> hid(n);  // dense haplotype index of each testcase (stack grouping)
+  int nth = n >= (1 << 16) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  if (threads > 0) nth = std::max(1, std::min(threads, n / 4096));
+  const size_t nn = std::max(n, 1);
+  host_reserve(b, nn, 0, nth);
+  // descriptors are written by the pack (a bigger pool than guessed grows the buffer after it)
+  if (int st = stage_reserve(b, StageLayout(nn, 32 * nn).total)) return st;
+  TcDesc *desc = (TcDesc *)b->h_stage;
+  uint32_t *hid = b->hid.data();  // dense haplotype index of each testcase (stack grouping)
   struct Chunk {
     int lo = 0, hi = 0;
-    std::vector<uint8_t> pool;
+    std::vector<uint8_t> *pool = nullptr;
     std::vector<uint32_t> hap_off;  // local haplotype id -> offset in this chunk's pool
     std::vector<HapKey> hap_key;    // local haplotype id -> key
-    int max_h = 0;
     int64_t cells = 0;
   };
-  const int nth = n >= (1 << 16) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
   std::vector<Chunk> ch(nth);
   auto pack_chunk = [&](Chunk &C) {
     std::unordered_map<ReadKey, uint32_t, KeyHash> read_at;
@@ -1064,28 +1113,30 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       uint32_t id = 0;
     };
     HapSlot hcache[256];
-    std::vector<uint8_t> &pool = C.pool;
+    std::vector<uint8_t> &pool = *C.pool;
     for (int k = C.lo; k < C.hi; k++) {
       const gb_testcase &t = tcs[k];
       const ReadKey rk{t.rs, t.q, t.i, t.d, t.c, t.rslen};
       uint32_t roff;
-      auto ri = rk == last_rk ? read_at.end() : read_at.find(rk);
       if (rk == last_rk) {
         roff = last_roff;
-      } else if (ri != read_at.end()) {
-        roff = ri->second;
       } else {
-        roff = (uint32_t)pool.size();
-        pool.resize(pool.size() + 5 * (size_t)t.rslen);
-        uint8_t *rec = pool.data() + roff;
-        for (int r = 0; r < t.rslen; r++) {
-          rec[r] = read_match_mask(base_code(t.rs[r]));
-          rec[t.rslen + r] = (uint8_t)t.q[r];
-          rec[2 * t.rslen + r] = (uint8_t)t.i[r];
-          rec[3 * t.rslen + r] = (uint8_t)t.d[r];
-          rec[4 * t.rslen + r] = (uint8_t)t.c[r];
+        auto ri = read_at.find(rk);
+        if (ri != read_at.end()) {
+          roff = ri->second;
+        } else {
+          roff = (uint32_t)pool.size();
+          pool.resize(pool.size() + 5 * (size_t)t.rslen);
+          uint8_t *rec = pool.data() + roff;
+          for (int r = 0; r < t.rslen; r++) {
+            rec[r] = read_match_mask(base_code(t.rs[r]));
+            rec[t.rslen + r] = (uint8_t)t.q[r];
+            rec[2 * t.rslen + r] = (uint8_t)t.i[r];
+            rec[3 * t.rslen + r] = (uint8_t)t.d[r];
+            rec[4 * t.rslen + r] = (uint8_t)t.c[r];
+          }
+          read_at.emplace(rk, roff);
         }
-        read_at.emplace(rk, roff);
       }
       last_rk = rk;
       last_roff = roff;
@@ -1112,16 +1163,16 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
         hs.id = id;
       }
       hid[k] = id;  // local until the merge
-      desc[k].read_off = roff;  // chunk-relative until the merge
-      desc[k].dims = (uint32_t)t.rslen | ((uint32_t)t.haplen << 16);
-      desc[k].out_idx = (uint32_t)k;
-      C.max_h = std::max(C.max_h, t.haplen);
+      // read offset chunk-relative and the local haplotype id until the merge
+      desc[k] = TcDesc{roff, 0, (uint32_t)t.rslen | ((uint32_t)t.haplen << 16), (uint32_t)k};
       C.cells += (int64_t)t.rslen * t.haplen;
     }
   };
   for (int t = 0; t < nth; t++) {
     ch[t].lo = (int)((int64_t)n * t / nth);
     ch[t].hi = (int)((int64_t)n * (t + 1) / nth);
+    ch[t].pool = &b->pools[t];
+    ch[t].pool->clear();
   }
   if (nth == 1) {
     pack_chunk(ch[0]);
@@ -1132,10 +1183,15 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     for (auto &x : th) x.join();
   }
   clk.mark("pack");
-  // merge: chunk pool bases, global haplotype ids (first appearance), one pool
+  // merge: chunk pool bases, global haplotype ids (first appearance), one pool in the staging buffer
   std::vector<size_t> base(nth + 1, 0);
-  for (int t = 0; t < nth; t++) base[t + 1] = base[t] + ch[t].pool.size();
+  for (int t = 0; t < nth; t++) base[t + 1] = base[t] + ch[t].pool->size();
   GB_ARG(base[nth] < (1ull << 32), "batch pool exceeds 4 GiB");
+  const size_t pool_bytes = std::max<size_t>((base[nth] + 15) & ~size_t(15), 16);
+  const StageLayout L(nn, pool_bytes);
+  if (int st = stage_reserve(b, L.total, sizeof(TcDesc) * nn)) return st;
+  desc = (TcDesc *)b->h_stage;
+  uint8_t *h_pool = b->h_stage + L.o_pool;
   std::vector<uint32_t> hap_off_of;
   std::vector<std::vector<uint32_t>> gid(nth);
   {
@@ -1152,15 +1208,10 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       }
     }
   }
-  std::vector<uint8_t> pool(base[nth]);
-  int max_h = 0;
   int64_t cells = 0;
-  for (int t = 0; t < nth; t++) {
-    max_h = std::max(max_h, ch[t].max_h);
-    cells += ch[t].cells;
-  }
+  for (int t = 0; t < nth; t++) cells += ch[t].cells;
   auto merge_chunk = [&](int t) {
-    if (!ch[t].pool.empty()) std::memcpy(pool.data() + base[t], ch[t].pool.data(), ch[t].pool.size());
+    if (!ch[t].pool->empty()) std::memcpy(h_pool + base[t], ch[t].pool->data(), ch[t].pool->size());
     for (int k = ch[t].lo; k < ch[t].hi; k++) {
       hid[k] = gid[t][hid[k]];
       desc[k].read_off += (uint32_t)base[t];
@@ -1175,19 +1226,19 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
     merge_chunk(0);
     for (auto &x : th) x.join();
   }
+  std::memset(h_pool + base[nth], 0, pool_bytes - base[nth]);
   clk.mark("merge");
   // Stacks (phmm_stack): testcases grouped by haplotype, stacked up to kStackRows rows (R + 2 per
   // testcase) and 64 testcases; longest-processing-time first (the dispatcher hands out workgroups
   // in grid order).
-  std::vector<int> order(n);
+  uint32_t *order = (uint32_t *)(b->h_stage + L.o_tc);  // the stacks' testcase lists
   {  // counting sort by haplotype (stable: testcases keep their order within a haplotype)
     std::vector<int> first(hap_off_of.size() + 1, 0);
     for (int k = 0; k < n; k++) first[hid[k] + 1]++;
     for (size_t h = 0; h < hap_off_of.size(); h++) first[h + 1] += first[h];
-    for (int k = 0; k < n; k++) order[first[hid[k]]++] = k;
+    for (int k = 0; k < n; k++) order[first[hid[k]]++] = (uint32_t)k;
   }
-  std::vector<Stack> stacks;
-  std::vector<uint64_t> scost;
+  clk.mark("haplotype order");
   // Stack height adapts to the job: tall stacks waste the least on partial stripes, but a job of
   // fewer than ~4 stacks per resident wave (32 per CU) leaves the grid's tail -- one whole stack --
   // exposed, and the f64 pass's persistent grid balances finer pieces better. Measured on the 'large'
@@ -1209,6 +1260,12 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
   int stack_rows = kStackRows;
   while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
+  // sort keys: long-haplotype stacks last (they run on the kLong kernels), then decreasing cost,
+  // then stack index (so the order is the stable one)
+  Stack *stacks = b->stacks.data();
+  uint64_t *key = b->skeys.data(), *key2 = key + nn;
+  int ns_all = 0, n_long = 0, max_h_short = 0, max_h_long = 0;
+  const int sh = b->rpl == 2 ? kRows2 : kWave;  // stripe height of the f32 pass
   for (int k = 0; k < n;) {
     const uint32_t h = desc[order[k]].hap_off;
     const int C = (int)(desc[order[k]].dims >> 16);
@@ -1220,38 +1277,40 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       S.count++;
       k++;
     }
-    stacks.push_back(S);
-    const int sh = b->rpl == 2 ? kRows2 : kWave;  // stripe height of the f32 pass
-    scost.push_back((uint64_t)((rows + sh - 1) / sh) * (uint64_t)(C + sh));
-  }
-  // by decreasing cost (stable), the stacks whose haplotype does not fit the LDS behind the others
-  // (they run on the kLong kernels)
-  std::vector<Stack> sorted_stacks(stacks.size());
-  int n_long = 0, max_h_short = 0, max_h_long = 0;
-  {
-    std::vector<uint32_t> idx(stacks.size());
-    for (size_t k = 0; k < idx.size(); k++) {
-      idx[k] = (uint32_t)k;
-      const int C = (int)stacks[k].C;
-      if (C > kLdsHaplen) {
-        n_long++;
-        max_h_long = std::max(max_h_long, C);
-      } else {
-        max_h_short = std::max(max_h_short, C);
-      }
+    const bool is_long = C > kLdsHaplen;
+    if (is_long) {
+      n_long++;
+      max_h_long = std::max(max_h_long, C);
+    } else {
+      max_h_short = std::max(max_h_short, C);
     }
-    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
-      const bool la = stacks[a].C > (uint32_t)kLdsHaplen, lb = stacks[b].C > (uint32_t)kLdsHaplen;
-      return la != lb ? lb : scost[a] > scost[b];
-    });
-    for (size_t k = 0; k < idx.size(); k++) sorted_stacks[k] = stacks[idx[k]];
+    const uint64_t cost = std::min<uint64_t>((uint64_t)((rows + sh - 1) / sh) * (uint64_t)(C + sh), 0x7fffffffu);
+    key[ns_all] = ((uint64_t)is_long << 63) | ((0x7fffffffu - cost) << 32) | (uint32_t)ns_all;
+    stacks[ns_all++] = S;
   }
-  std::vector<uint32_t> stk_tc(order.begin(), order.end());
-  if (pool.empty()) pool.resize(4);
-  pool.resize((pool.size() + 15) & ~size_t(15));
-
+  clk.mark("stack build");
+  {  // LSD radix sort of the keys' upper 32 bits, 8 bits a pass (the low 32 bits are the index)
+    uint32_t cnt[256];
+    for (int shift = 32; shift < 64; shift += 8) {
+      const uint64_t d0 = ns_all ? (key[0] >> shift) & 255 : 0;
+      bool same = true;
+      for (int k = 1; k < ns_all && same; k++) same = ((key[k] >> shift) & 255) == d0;
+      if (same) continue;
+      std::memset(cnt, 0, sizeof(cnt));
+      for (int k = 0; k < ns_all; k++) cnt[(key[k] >> shift) & 255]++;
+      for (uint32_t d = 0, sum = 0; d < 256; d++) {
+        const uint32_t c = cnt[d];
+        cnt[d] = sum;
+        sum += c;
+      }
+      for (int k = 0; k < ns_all; k++) key2[cnt[(key[k] >> shift) & 255]++] = key[k];
+      std::swap(key, key2);
+    }
+  }
+  Stack *h_stacks = (Stack *)(b->h_stage + L.o_stk);
+  for (int k = 0; k < ns_all; k++) h_stacks[k] = stacks[(uint32_t)key[k]];
   clk.mark("stacks");
-  if (int st = batch_reserve(b, n, pool.size())) return st;
+  if (int st = batch_reserve(b, n, pool_bytes)) return st;
   if (n_long) {
     // records + codes of one long stack per workgroup of the persistent kLong grid
     b->long_grid = std::min(n_long, b->f64_grid);
@@ -1266,34 +1325,21 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n) {
       b->cap_scratch = need;
     }
   }
-  // the uploads go through the batch's pinned staging buffer: a pageable copy is staged by the
-  // runtime, and while an earlier chunk's kernels held the GPU one chunk's upload waited 10-15 ms
-  // for it (profiles/r05j_phmm_cli.log); a pinned copy is a plain DMA
-  {
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t o1 = up(sizeof(TcDesc) * n), o2 = o1 + up(sizeof(uint32_t) * n),
-                 o3 = o2 + up(sizeof(Stack) * sorted_stacks.size()), tot = o3 + pool.size();
-    if (int st = stage_reserve(b, tot)) return st;
-    uint8_t *h = b->h_stage;
-    if (n) {
-      std::memcpy(h, desc.data(), sizeof(TcDesc) * n);
-      std::memcpy(h + o1, stk_tc.data(), sizeof(uint32_t) * n);
-      std::memcpy(h + o2, sorted_stacks.data(), sizeof(Stack) * sorted_stacks.size());
-      GB_HIP(hipMemcpyAsync(b->d_desc, h, sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
-      GB_HIP(hipMemcpyAsync(b->d_stk_tc, h + o1, sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
-      GB_HIP(hipMemcpyAsync(b->d_stacks, h + o2, sizeof(Stack) * sorted_stacks.size(), hipMemcpyHostToDevice,
-                            b->stream));
-    }
-    std::memcpy(h + o3, pool.data(), pool.size());
-    GB_HIP(hipMemcpyAsync(b->d_pool, h + o3, pool.size(), hipMemcpyHostToDevice, b->stream));
+  // the uploads go through the pinned staging buffer: a pageable copy is staged by the runtime, and
+  // while an earlier chunk's kernels held the GPU one chunk's upload waited 10-15 ms for it
+  // (profiles/r05j_phmm_cli.log); a pinned copy is a plain DMA
+  if (n) {
+    GB_HIP(hipMemcpyAsync(b->d_desc, desc, sizeof(TcDesc) * n, hipMemcpyHostToDevice, b->stream));
+    GB_HIP(hipMemcpyAsync(b->d_stk_tc, order, sizeof(uint32_t) * n, hipMemcpyHostToDevice, b->stream));
+    GB_HIP(hipMemcpyAsync(b->d_stacks, h_stacks, sizeof(Stack) * ns_all, hipMemcpyHostToDevice, b->stream));
   }
+  GB_HIP(hipMemcpyAsync(b->d_pool, h_pool, pool_bytes, hipMemcpyHostToDevice, b->stream));
   GB_HIP(hipStreamSynchronize(b->stream));  // the staging buffer is reused by the next fill
   clk.mark("upload");
   b->n = n;
-  b->nstacks = (int)sorted_stacks.size() - n_long;
+  b->nstacks = ns_all - n_long;
   b->n_long = n_long;
   b->max_haplen = max_h_short;
-  (void)max_h;
   b->cells = cells;
   b->ran = false;
   return GB_OK;
@@ -1360,14 +1406,31 @@ int warm_up(DeviceTables *t) {
     GB_HIP(hipEventRecord(w->ev[0], w->stream));
   }
   for (int c = 1; c < kPipeMaxChunks; c++) GB_HIP(hipStreamSynchronize(thread_workspace(t, &st, c)->stream));
+  // buffers for a job of GB_PHMM_PREALLOC testcases (default 1 M; 0: none) in the pipeline's chunk
+  // proportions: allocating them inside the first call cost bin/phmm ~14 ms of its timed region
+  // (device ~90 B, pinned ~70 B and host scratch ~70 B per testcase; all grow on demand past it)
+  int64_t pre = 1 << 20;
+  if (const char *e = getenv("GB_PHMM_PREALLOC")) pre = std::max(0ll, atoll(e));
+  if (pre > 0) {
+    const int64_t W = (int64_t)kPipeMaxChunks * (kPipeMaxChunks + 1) / 2;
+    for (int c = 0; c < kPipeMaxChunks; c++) {
+      gb_phmm_batch *w = thread_workspace(t, &st, c);
+      const int64_t m = pre * (c + 1) / W + 1;
+      const size_t pool = 32 * (size_t)m;
+      if ((st = batch_reserve(w, (int)std::min<int64_t>(m, 1 << 30), pool))) return st;
+      if ((st = stage_reserve(w, StageLayout((size_t)m, pool).total))) return st;
+      host_reserve(w, (size_t)m, pool, 4);
+    }
+  }
   return GB_OK;
 }
 
-// Pipelined one-call path for big calls: the testcases are cut into contiguous chunks, each packed
-// into its own workspace batch (own stream) and launched as soon as it is packed, so packing chunk
-// c + 1 on the host overlaps the kernels of chunk c, and chunk c's results (D2H + log10) overlap the
-// kernels of the chunks after it. Chunks are independent jobs, so results are those of one job.
-
+// Pipelined one-call path for big calls: the testcases are cut into contiguous chunks of growing size
+// (weights 1, 2, .., k), each packed into its own workspace batch (own stream). The first, small
+// chunk is packed on the calling thread and launched at once; the others are packed meanwhile on
+// worker threads and launched in order as they become ready, so the host's packing hides behind the
+// kernels, and chunk c's results (D2H + log10) overlap the kernels of the chunks after it. Chunks are
+// independent jobs, so results are those of one job.
 int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double *results, float *raw_f,
                       double *raw_d, uint8_t *used_double) {
   const char *e = getenv("GB_PHMM_PIPE");  // probes: the chunk count (1 = one job, no overlap)
@@ -1375,49 +1438,45 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
   if (e) k = std::max(1, std::min(16, atoi(e)));
   std::vector<gb_phmm_batch *> B(k);
   std::vector<int> lo(k + 1);
-  for (int c = 0; c <= k; c++) lo[c] = (int)((int64_t)n * c / k);
+  const int64_t W = (int64_t)k * (k + 1) / 2;
+  for (int c = 0; c <= k; c++) lo[c] = (int)((int64_t)n * ((int64_t)c * (c + 1) / 2) / W);
   int st = GB_OK;
   for (int c = 0; c < k; c++) {
     B[c] = thread_workspace(tabs, &st, c);
     if (!B[c]) return st;
     B[c]->force_f64 = false;
   }
-  // every chunk's per-testcase device arrays and a pinned staging buffer first, so few allocations
-  // run while an earlier chunk computes. The pool is estimated as the reads that change from one
-  // testcase to the next (the reference's r-major order) plus the haplotypes not seen lately;
-  // batch_fill grows both buffers should the packed pool be larger.
-  for (int c = 0; c < k; c++) {
-    size_t pool_bytes = 16;
-    const char *prev_rs = nullptr;
-    const char *hseen[512] = {};  // direct-mapped: a collision only overestimates
-    for (int t = lo[c]; t < lo[c + 1]; t++) {
-      if (tcs[t].rs != prev_rs) {
-        pool_bytes += 5 * (size_t)std::max(tcs[t].rslen, 0);
-        prev_rs = tcs[t].rs;
-      }
-      const size_t hs = ((uintptr_t)tcs[t].hap >> 4) % 512;
-      if (hseen[hs] != tcs[t].hap) {
-        hseen[hs] = tcs[t].hap;
-        pool_bytes += (size_t)std::max(tcs[t].haplen, 0);
-      }
-    }
-    pool_bytes = (pool_bytes + pool_bytes / 4 + 15) & ~(size_t)15;
-    const int m = lo[c + 1] - lo[c];
-    if ((st = batch_reserve(B[c], m, pool_bytes))) return st;
-    if ((st = stage_reserve(B[c], 36 * (size_t)m + 1024 + pool_bytes))) return st;
-  }
   HostClock clk;
+  // host threads: about 12 over the concurrent fills (GB_PHMM_FILL_THREADS: per fill)
+  int fill_threads = std::max(1, 12 / k);
+  if (const char *f = getenv("GB_PHMM_FILL_THREADS")) fill_threads = std::max(1, atoi(f));
+  const int device = tabs->device;
+  auto fill = [&, device](int c) -> std::pair<int, std::string> {
+    if (hipSetDevice(device) != hipSuccess) return {GB_ERR_HIP, "gb_phmm_compute: hipSetDevice failed"};
+    const int s = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c], fill_threads);
+    return {s, s ? std::string(gb::last_error()) : std::string()};
+  };
+  // the workers' futures join on destruction, also on an early return
+  std::vector<std::future<std::pair<int, std::string>>> ready;
+  for (int c = 1; c < k; c++) ready.push_back(std::async(std::launch::async, fill, c));
   auto fetch = [&](int c) {
     const int o = lo[c];
     return gb_phmm_batch_results(B[c], results ? results + o : nullptr, raw_f ? raw_f + o : nullptr,
                                  raw_d ? raw_d + o : nullptr, used_double ? used_double + o : nullptr, nullptr);
   };
+  if ((st = batch_fill(B[0], tcs, lo[1], fill_threads))) return st;
+  clk.mark("chunk 0 filled");
+  if ((st = gb_phmm_batch_run(B[0]))) return st;
   // chunk c - 2's results are fetched after chunk c is launched: the host never waits on the chunk
-  // the GPU has just started, only on one queued behind it, and packs ahead meanwhile
+  // the GPU has just started, only on one queued behind it
   int fetched = 0;
-  for (int c = 0; c < k; c++) {
-    if ((st = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c]))) return st;
-    clk.mark("chunk filled");
+  for (int c = 1; c < k; c++) {
+    const auto r = ready[c - 1].get();
+    if (r.first) {
+      gb::set_error("%s", r.second.c_str());
+      return r.first;
+    }
+    clk.mark("chunk ready");
     if ((st = gb_phmm_batch_run(B[c]))) return st;
     if (c >= 2) {
       if ((st = fetch(fetched++))) return st;
@@ -1530,10 +1589,27 @@ int gb_phmm_batch_results(gb_phmm_batch *b, double *results, float *raw_f, doubl
   GB_HIP(hipStreamSynchronize(b->stream));
   const int n = b->n;
   if (n == 0) return GB_OK;
-  std::vector<float> rf(n);
-  std::vector<double> rd(n);
-  GB_HIP(hipMemcpy(rf.data(), b->d_rf, sizeof(float) * n, hipMemcpyDeviceToHost));
-  GB_HIP(hipMemcpy(rd.data(), b->d_rd, sizeof(double) * n, hipMemcpyDeviceToHost));
+  // raw likelihoods back through the pinned staging buffer when it is big enough (a pageable copy is
+  // staged by the runtime)
+  std::vector<float> rf_v;
+  std::vector<double> rd_v;
+  const float *rf;
+  const double *rd;
+  const size_t off_d = (sizeof(float) * (size_t)n + 255) & ~(size_t)255;
+  if (b->h_stage && b->cap_stage >= off_d + sizeof(double) * (size_t)n) {
+    GB_HIP(hipMemcpyAsync(b->h_stage, b->d_rf, sizeof(float) * n, hipMemcpyDeviceToHost, b->stream));
+    GB_HIP(hipMemcpyAsync(b->h_stage + off_d, b->d_rd, sizeof(double) * n, hipMemcpyDeviceToHost, b->stream));
+    GB_HIP(hipStreamSynchronize(b->stream));
+    rf = (const float *)b->h_stage;
+    rd = (const double *)(b->h_stage + off_d);
+  } else {
+    rf_v.resize(n);
+    rd_v.resize(n);
+    GB_HIP(hipMemcpy(rf_v.data(), b->d_rf, sizeof(float) * n, hipMemcpyDeviceToHost));
+    GB_HIP(hipMemcpy(rd_v.data(), b->d_rd, sizeof(double) * n, hipMemcpyDeviceToHost));
+    rf = rf_v.data();
+    rd = rd_v.data();
+  }
   if (dev_results) GB_HIP(hipMemcpy(dev_results, b->d_out, sizeof(double) * n, hipMemcpyDeviceToHost));
   const float l10f = b->tabs->hf.log10_init;
   const double l10d = b->tabs->hd.log10_init;

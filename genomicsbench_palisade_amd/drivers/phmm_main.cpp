@@ -18,6 +18,7 @@
 #include <fstream>
 #include <iostream>
 #include <string>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -86,10 +87,13 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
   // spread over a few host threads at precomputed offsets
   std::vector<size_t> off(shard.size() + 1, 0);
   for (size_t k = 0; k < shard.size(); k++) off[k + 1] = off[k] + shard[k]->reads.size() * shard[k]->haps.size();
-  std::vector<gb_testcase> tcs(off.back());
+  // not value-initialised: the build threads touch the pages first (a zero fill of the ~50 MB array
+  // of the 'large' job cost a few ms of the timed region on one thread)
+  const size_t ntc = off.back();
+  std::unique_ptr<gb_testcase[]> tcs(new gb_testcase[std::max<size_t>(ntc, 1)]);
   auto build = [&](size_t k0, size_t k1) {
     for (size_t k = k0; k < k1; k++) {
-      gb_testcase *t = tcs.data() + off[k];
+      gb_testcase *t = tcs.get() + off[k];
       for (auto &r : shard[k]->reads)
         for (auto &h : shard[k]->haps) {
           t->rslen = (int)r.bases.size();
@@ -112,7 +116,7 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
     for (size_t t = 0; t < nth; t++) th.emplace_back(build, shard.size() * t / nth, shard.size() * (t + 1) / nth);
     for (auto &x : th) x.join();
   }
-  std::vector<double> res(tcs.size());
+  std::unique_ptr<double[]> res(new double[std::max<size_t>(ntc, 1)]);
   if (getenv("GB_PHMM_HOSTPROF")) {
     struct timeval tb;
     gettimeofday(&tb, nullptr);
@@ -121,19 +125,19 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
   }
   if (loops == 1) {
     // one pass: gb_phmm_compute pipelines big jobs (packing chunk c + 1 while chunk c computes)
-    st = gb_phmm_compute(tcs.data(), (int)tcs.size(), res.data(), nullptr, nullptr, nullptr);
+    st = gb_phmm_compute(tcs.get(), (int)ntc, res.get(), nullptr, nullptr, nullptr);
     if (st) die("gb_phmm_compute", st);
     gettimeofday(&t1, nullptr);
   } else {
     // -l N: the job is packed once and stays on the device for the N passes
     gb_phmm_batch *job = nullptr;
-    st = gb_phmm_batch_create(tcs.data(), (int)tcs.size(), &job);
+    st = gb_phmm_batch_create(tcs.get(), (int)ntc, &job);
     if (st) die("gb_phmm_batch_create", st);
     for (int l = 0; l < loops; l++) {
       st = gb_phmm_batch_run(job);
       if (st) die("gb_phmm_batch_run", st);
     }
-    st = gb_phmm_batch_results(job, res.data(), nullptr, nullptr, nullptr, nullptr);
+    st = gb_phmm_batch_results(job, res.get(), nullptr, nullptr, nullptr, nullptr);
     if (st) die("gb_phmm_batch_results", st);
     gettimeofday(&t1, nullptr);
     gb_phmm_batch_destroy(job);
