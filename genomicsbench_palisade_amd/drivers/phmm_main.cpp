@@ -9,6 +9,7 @@
 // per device, no collective). Prints the reference's closing line "PairHMM completed. Kernel
 // runtime: X sec"; -p prints every result like PRINT_OUTPUT ("%lf").
 #include <getopt.h>
+#include <sys/mman.h>
 #include <sys/time.h>
 
 #include <algorithm>
@@ -66,6 +67,27 @@ bool read_batch(std::istream &is, Batch &b) {
   return true;
 }
 
+// uninitialised array of n T on transparent huge pages where the kernel allows them: the build threads
+// fault it in 2 MiB at a time instead of 4 KiB
+template <typename T>
+struct BigArray {
+  T *p = nullptr;
+  explicit BigArray(size_t n) {
+    const size_t huge = 2u << 20, bytes = (std::max<size_t>(n, 1) * sizeof(T) + huge - 1) & ~(huge - 1);
+    p = (T *)std::aligned_alloc(huge, bytes);
+    if (!p) {
+      fprintf(stderr, "phmm: out of memory (%zu bytes)\n", bytes);
+      exit(EXIT_FAILURE);
+    }
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+  }
+  ~BigArray() { std::free(p); }
+  BigArray(const BigArray &) = delete;
+  BigArray &operator=(const BigArray &) = delete;
+  T *get() const { return p; }
+  T &operator[](size_t k) const { return p[k]; }
+};
+
 void die(const char *what, int st) {
   fprintf(stderr, "phmm: %s failed (%d): %s\n", what, st, gb_last_error());
   exit(EXIT_FAILURE);
@@ -90,7 +112,7 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
   // not value-initialised: the build threads touch the pages first (a zero fill of the ~50 MB array
   // of the 'large' job cost a few ms of the timed region on one thread)
   const size_t ntc = off.back();
-  std::unique_ptr<gb_testcase[]> tcs(new gb_testcase[std::max<size_t>(ntc, 1)]);
+  BigArray<gb_testcase> tcs(ntc);
   auto build = [&](size_t k0, size_t k1) {
     for (size_t k = k0; k < k1; k++) {
       gb_testcase *t = tcs.get() + off[k];
@@ -116,7 +138,7 @@ double run_shard(int device, std::vector<Batch *> shard, int loops) {
     for (size_t t = 0; t < nth; t++) th.emplace_back(build, shard.size() * t / nth, shard.size() * (t + 1) / nth);
     for (auto &x : th) x.join();
   }
-  std::unique_ptr<double[]> res(new double[std::max<size_t>(ntc, 1)]);
+  BigArray<double> res(ntc);
   if (getenv("GB_PHMM_HOSTPROF")) {
     struct timeval tb;
     gettimeofday(&tb, nullptr);
