@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-5 GPU call o: chain 'large' 1/8 shard step timeline (current code)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r05o}
+timeout -k 10 120 python -u tools/chain_shard_probe.py > gpurun_out/chain_shard_${T}.log 2>&1 || { tail -20 gpurun_out/chain_shard_${T}.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/chain_shard_${T}.log
+rm -rf gpurun_out/chain_shard_trace_${T}
+timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/chain_shard_trace_${T} -- \
+  python -u tools/chain_shard_probe.py > gpurun_out/chain_shard_trace_${T}.log 2>&1 || { tail -20 gpurun_out/chain_shard_trace_${T}.log; exit 1; }
+python tools/kernel_timeline.py gpurun_out/chain_shard_trace_${T} chain_rows > gpurun_out/chain_shard_timeline_${T}.txt
+cat gpurun_out/chain_shard_timeline_${T}.txt
+CHAIN_KIND=small timeout -k 10 120 python -u tools/chain_shard_probe.py > gpurun_out/chain_sshard_${T}.log 2>&1 || { tail -20 gpurun_out/chain_sshard_${T}.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/chain_sshard_${T}.log
