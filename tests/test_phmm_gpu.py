@@ -176,10 +176,12 @@ def test_stack_edges_vs_oracle(phmm, seed):
     assert (got[3].astype(bool) == exp[3].astype(bool)).all()
 
 
-@pytest.mark.parametrize("chunks", ["3", "1"])
+@pytest.mark.parametrize("chunks", ["3", "1", "6"])
 def test_pipelined_compute_bit_exact(phmm, monkeypatch, chunks):
-    """gb_phmm_compute's pipelined path (chunks packed and launched one after the other on their own
-    streams; GB_PHMM_PIPE forces it for a small call) gives the one-job results, against the oracle."""
+    """gb_phmm_compute's pipelined path (chunks of growing size, each on its own workspace and stream,
+    the first packed on the calling thread and the rest concurrently on worker threads; GB_PHMM_PIPE
+    forces it for a small call, 6 chunks use workspaces beyond the four gb_phmm_init reserves) gives
+    the one-job results, against the oracle."""
     monkeypatch.setenv("GB_PHMM_PIPE", chunks)
     rng = np.random.default_rng(23)
     ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(5)])
@@ -188,8 +190,47 @@ def test_pipelined_compute_bit_exact(phmm, monkeypatch, chunks):
     assert (got[3].astype(bool) == (got[1] < np.float32(1e-28))).all()
 
 
+def big_pool_job(seed=31, n=600):
+    """Every testcase its own long read: ~1.1 KB of packed pool per testcase, far above the 32 B per
+    testcase a fill reserves pinned staging for before its pack."""
+    rng = np.random.default_rng(seed)
+    haps = [gen.BASES[rng.integers(0, 4, k)].tobytes() for k in (300, 410, 77)]
+    return TestcaseArray.from_pairs([(_read(rng, int(m)), haps[k % 3])
+                                     for k, m in enumerate(rng.integers(150, 260, n))])
+
+
+def test_pipelined_fresh_workspaces_bit_exact(tmp_path):
+    """The first call of a process that reserved nothing at init (GB_PHMM_PREALLOC=0): every chunk's
+    fill allocates its device buffers and pinned staging while other chunks' fills and kernels run,
+    and the staging grows after the pack (keeping the descriptors already written) -- bit-exact
+    against the oracle, in a process of its own."""
+    out = tmp_path / "res.npz"
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r})\n"
+        "from genomicsbench_palisade_amd import phmm, set_device\n"
+        "import test_phmm_gpu as t\n"
+        "set_device(0); phmm.init_pairhmm()\n"
+        "r = phmm.compute_likelihoods_both(t.big_pool_job())\n"
+        f"np.savez({str(out)!r}, out=r[0], rf=r[1], rd=r[2], ud=r[3])\n")
+    env = dict(os.environ, GB_PHMM_PREALLOC="0", GB_PHMM_PIPE="3")
+    subprocess.run([os.sys.executable, "-c", code], env=env, check=True, timeout=240)
+    z = np.load(out)
+    ta = big_pool_job()
+    exp = oracle_run(ta)
+    assert_exact((z["out"], z["rf"], z["rd"]), exp)
+    assert (z["ud"].astype(bool) == exp[3].astype(bool)).all()
+
+
+def test_pipelined_big_pool_bit_exact(phmm, monkeypatch):
+    """The same shape in this process (workspaces reserved at init), other reads."""
+    monkeypatch.setenv("GB_PHMM_PIPE", "3")
+    ta = big_pool_job(seed=37)
+    assert_exact(phmm.compute_likelihoods_both(ta), oracle_run(ta))
+
+
 def test_rows_per_lane_ab_identical(phmm, monkeypatch):
-    """The f32 pass with two rows per lane (default) and with one (GB_PHMM_RPL=1) agree bit for bit
+    """The f32 pass with one row per lane (default) and with two (GB_PHMM_RPL=2) agree bit for bit
     on a job with many stacks, partial stripes and both passes."""
     rng = np.random.default_rng(29)
     ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 50, 20) for _ in range(4)])
