@@ -1240,10 +1240,13 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
   }
   clk.mark("haplotype order");
   // Stack height adapts to the job: tall stacks waste the least on partial stripes, but a job of
-  // fewer than ~4 stacks per resident wave (32 per CU) leaves the grid's tail -- one whole stack --
-  // exposed, and the f64 pass's persistent grid balances finer pieces better. Measured on the 'large'
-  // job's 1/8 strong-scaling shard (tools/phmm_shard_probe.py): 2048 rows 4.97 ms, 1024 4.51, 512 4.37,
-  // 256 4.64 per step; on the whole job 2048 rows stay best (33.0 ms; 512: 33.7).
+  // few stacks per resident wave leaves the grid's tail -- one whole stack -- exposed, and the f64
+  // pass's persistent grid balances finer pieces better. 2048 rows from 4 stacks per resident wave
+  // (32 per CU) up, 512 below 16 stacks per CU, 1024 between. Measured (tools/phmm_shard_probe.py,
+  // profiles/r05w_phmm_rows.log, r05x): the 'large' job 2048 / 1024 / 512 rows 32.3 / 32.6 / 33.6 ms,
+  // its 1/2, 1/4 and 1/8 shards best at 1024 (1/4: 8.57 ms against 8.76-8.80 at 512 / 2048; 1/8:
+  // 4.48 against 4.53 / 4.74), the 'small' job 1024 (4.27 against 4.41 at 512) and its 1/8 shard,
+  // 2.75 M rows, 512 (0.83 ms against 0.90 at 1024).
   int64_t total_rows = 0;
   for (int k = 0; k < n; k++) total_rows += (int64_t)(desc[k].dims & 0xffff) + 2;
   // one row per lane: the two-row form (phmm_forward2) issues 125 VALU per 8 cells against 67 per 4
@@ -1258,7 +1261,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
   b->f64_parts = 2;
   if (const char *e = getenv("GB_PHMM_F64_PARTS")) b->f64_parts = std::max(1, std::min(8, atoi(e)));
   int stack_rows = kStackRows;
-  while (stack_rows > 512 && total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows /= 2;
+  if (total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows = 1024;
+  if (stack_rows == 1024 && total_rows / stack_rows < 16ll * b->cus) stack_rows = 512;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
   // sort keys: long-haplotype stacks last (they run on the kLong kernels), then decreasing cost,
   // then stack index (so the order is the stable one)

@@ -12,7 +12,9 @@ from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: E402
 
 set_device(0)
 phmm.init_pairhmm()
-full = TestcaseArray.from_batches(gen.phmm_dataset("large", int(os.environ.get("PHMM_BATCHES", "64")), seed=1))
+# PHMM_KIND=small: the 'small'-shaped job
+full = TestcaseArray.from_batches(gen.phmm_dataset(os.environ.get("PHMM_KIND", "large"),
+                                                   int(os.environ.get("PHMM_BATCHES", "64")), seed=1))
 of, r = int(os.environ.get("PHMM_OF", "8")), int(os.environ.get("PHMM_RANK", "0"))
 for name, ta in [("full", full), (f"shard {r}/{of}", shard.shard_testcases(full, r, of)[0])]:
     for rows in os.environ.get("PHMM_ROWS", "default").split(";"):
