@@ -1084,8 +1084,13 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
     GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
   }
   clk.mark("validate");
-  int nth = n >= (1 << 16) ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  // calls from 8 K testcases pack on several threads (2 K testcases each at least): the reference's
+  // per-batch calls (PairHMMUnitTest.cpp:549-593) are mostly 5-45 K testcases
+  int pack_min = 1 << 13;  // GB_PHMM_PACK_MIN (probes): the smallest call packed on several threads
+  if (const char *e = getenv("GB_PHMM_PACK_MIN")) pack_min = std::max(1, atoi(e));
+  int nth = n >= pack_min ? (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
   if (threads > 0) nth = std::max(1, std::min(threads, n / 4096));
+  nth = std::max(1, std::min(nth, n / 2048));
   const size_t nn = std::max(n, 1);
   host_reserve(b, nn, 0, nth);
   // descriptors are written by the pack (a bigger pool than guessed grows the buffer after it)
@@ -1263,6 +1268,9 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
   int stack_rows = kStackRows;
   if (total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows = 1024;
   if (stack_rows == 1024 && total_rows / stack_rows < 16ll * b->cus) stack_rows = 512;
+  // a small call (one of the reference's per-batch calls) is its longest stack: below 2 stacks per
+  // SIMD the stacks shrink further, to 128 rows
+  while (stack_rows > 128 && total_rows / stack_rows < 8ll * b->cus) stack_rows /= 2;
   if (const char *e = getenv("GB_PHMM_STACK_ROWS")) stack_rows = std::max(1, atoi(e));  // probes
   // sort keys: long-haplotype stacks last (they run on the kLong kernels), then decreasing cost,
   // then stack index (so the order is the stable one)
@@ -1384,7 +1392,8 @@ gb_phmm_batch *thread_workspace(DeviceTables *tabs, int *st, int slot = 0) {
   return b;
 }
 
-constexpr int kPipeMinChunk = 65536;  // testcases per chunk at least
+constexpr int kPipeMinChunk = 65536;  // testcases per chunk from three chunks on
+constexpr int kPipeMin2 = 16384;      // the smallest call pipelined (two chunks)
 constexpr int kPipeMaxChunks = 4;
 
 // gb_phmm_init (the reference's initPairHMM, called before its timed loop) also readies what the
@@ -1438,7 +1447,8 @@ int warm_up(DeviceTables *t) {
 int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double *results, float *raw_f,
                       double *raw_d, uint8_t *used_double) {
   const char *e = getenv("GB_PHMM_PIPE");  // probes: the chunk count (1 = one job, no overlap)
-  int k = std::min(kPipeMaxChunks, std::max(1, n / kPipeMinChunk));
+  // two chunks from kPipeMin2 testcases (the reference's bigger per-batch calls), up to four
+  int k = std::min(kPipeMaxChunks, std::max(2, n / kPipeMinChunk));
   if (e) k = std::max(1, std::min(16, atoi(e)));
   std::vector<gb_phmm_batch *> B(k);
   std::vector<int> lo(k + 1);
@@ -1689,7 +1699,7 @@ int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f
   DeviceTables *tabs = nullptr;
   int st = get_device_tables(&tabs);
   if (st) return st;
-  if (n >= 2 * kPipeMinChunk || getenv("GB_PHMM_PIPE"))
+  if (n >= kPipeMin2 || getenv("GB_PHMM_PIPE"))
     return compute_pipelined(tabs, tcs, n, results, raw_f, raw_d, used_double);
   gb_phmm_batch *b = thread_workspace(tabs, &st);
   if (!b) return st;
