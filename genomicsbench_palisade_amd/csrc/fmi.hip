@@ -176,6 +176,15 @@ static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
 // forward phase the slots hold the last kTop pushes (a push evicts the one kTop before it to its
 // scratch position), and the compaction writes r'[q] into r[q]'s slot, already read. 8 KB per wave
 // beside the 5.25 KB of staged read codes: 12 waves per CU still fit.
+// slot of a ring of N entries (N a power of two: a mask; 6: an unsigned modulo, x >= 0)
+template <int N>
+__device__ __forceinline__ int ring_slot(int x) {
+  if constexpr ((N & (N - 1)) == 0)
+    return x & (N - 1);
+  else
+    return (int)((unsigned)x % (unsigned)N);
+}
+
 template <bool kLdsQ, int kTop>  // kTop 0: every entry in the scratch
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   constexpr bool kTopLds = kTop > 0;
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
     const PEnt pe = pack_ent(e);
     if constexpr (kTopLds) {
       const int k = numPrev;
-      PEnt *slot = top + (size_t)(k & (kTop - 1)) * 64;
+      PEnt *slot = top + (size_t)ring_slot<kTop>(k) * 64;
       if (k >= kTop) prev.base[(size_t)(L - 1 - (k - kTop)) * 64] = *slot;
       *slot = pe;
     } else {
@@ -231,13 +240,13 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   // list index p of the current reversed list (p >= 1; r[0] is `head`)
   auto get_r = [&](int p_) -> PEnt {
     if constexpr (kTopLds)
-      if (p_ < kTop) return top[(size_t)((tc - p_) & (kTop - 1)) * 64];
+      if (p_ < kTop) return top[(size_t)ring_slot<kTop>(tc - p_) * 64];
     return prev.base[(size_t)(r0 + p_) * 64];
   };
   auto put_r = [&](int q_, const PEnt &pe) {
     if constexpr (kTopLds)
       if (q_ < kTop) {
-        top[(size_t)((tc - q_) & (kTop - 1)) * 64] = pe;
+        top[(size_t)ring_slot<kTop>(tc - q_) * 64] = pe;
         return;
       }
     prev.base[(size_t)(r0 + q_) * 64] = pe;
@@ -929,20 +938,24 @@ int device_cus() {
   return cus;
 }
 
-// `prev` list head entries kept in LDS (GB_FMI_TOP: 8, 4 or 0)
+// `prev` list head entries kept in LDS (GB_FMI_TOP: 0, 4-8). Five (9.9 KB per wave with the staged
+// read codes, 16 waves per CU still fit): 10 M reads 243.9 -> 232.7 ms, the 1/8 shard 35.2 -> 34.0 ms
+// against four; six at 14 / 15 waves 233.8, seven at 13 249.7, eight at 11 259.6
+// (profiles/r05zi_fmi_top.log)
 int top_entries() {
   const char *te = getenv("GB_FMI_TOP");
-  return te ? atoi(te) : 4;
+  return te ? atoi(te) : 5;
 }
 
 int lanes_for_device(int cus) {
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
   // Waves (workgroups) per CU of the persistent grid. LDS per wave is the staged read codes (4.9 KB)
-  // plus the `prev` list head (2 KB per entry kept); 116 VGPRs allow 4 waves per SIMD. With an
-  // 8-entry head (13 KB) 12 fit and 11 / 12 run alike; a 4-entry head (8.9 KB) lets the VGPR limit,
-  // 16, bind, which hides more gather latency than the 4 extra LDS entries save: 10 M reads 248 vs
-  // 260 ms, the 1/8 shard 35.8 vs 36.7 ms (tools/fmi_knob_probe.py, profiles/r04e_fmi_knobs.log).
-  const int waves = e ? std::max(1, atoi(e)) : (top_entries() >= 8 ? 11 : 16);
+  // plus the `prev` list head (1 KB per entry kept); 116 VGPRs allow 4 waves per SIMD. With an
+  // 8-entry head (13 KB) 12 fit and 11 / 12 run alike; a 4- or 5-entry head (8.9 / 9.9 KB) lets the
+  // VGPR limit, 16, bind, which hides more gather latency than extra LDS entries save (round 4: 10 M
+  // reads 248 vs 260 ms at 4 / 8 entries, profiles/r04e_fmi_knobs.log; round 5: top_entries).
+  const int top = top_entries();
+  const int waves = e ? std::max(1, atoi(e)) : (top >= 8 ? 11 : top >= 7 ? 13 : top >= 6 ? 14 : 16);
   return cus * waves * 64;
 }
 
@@ -1364,6 +1377,12 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0')) {
       if (top >= 8)
         launch(gbfmi::smem_search<true, 8>);
+      else if (top >= 7)
+        launch(gbfmi::smem_search<true, 7>);
+      else if (top >= 6)
+        launch(gbfmi::smem_search<true, 6>);
+      else if (top >= 5)
+        launch(gbfmi::smem_search<true, 5>);
       else if (top >= 4)
         launch(gbfmi::smem_search<true, 4>);
       else

@@ -78,6 +78,25 @@ def test_search_vs_oracle_exact(fmi, tmp_path, size, nreads, L, seed):
     assert calls == oi.bwt_calls()  # identical work: the same backwardExt calls
 
 
+@pytest.mark.parametrize("top", ["0", "4", "5", "6", "7", "8"])
+def test_prev_head_sizes_exact(fmi, monkeypatch, top):
+    """The `prev` list head kept in LDS (GB_FMI_TOP entries: a ring of the last pushes, a power of two
+    masked, 5 / 6 / 7 by an unsigned modulo) on reads in repeats, whose lists grow long and are
+    compacted through the head: SMEMs, counts and backwardExt calls equal the oracle's."""
+    monkeypatch.setenv("GB_FMI_TOP", top)
+    ref = gen.fmi_reference(300_000, seed=41, repeat_frac=0.3)
+    codes, lens = gen.fmi_reads(ref, 2500, read_len=151, seed=42, sub_rate=0.03, n_rate=0.002)
+    oi = fmi_util.OracleIndex(ref)
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512)
+    idx = fmi.Index.build(ref)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(19)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    assert tot == len(exp) and (bc == ebc).all() and (pc == epc).all()
+    assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
+    assert rs.timing()[2] == oi.bwt_calls()
+
+
 def test_search_repeat_runs_identical(fmi):
     ref = gen.fmi_reference(100_000, seed=9)
     codes, lens = gen.fmi_reads(ref, 1500, seed=10)
