@@ -7,6 +7,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import genomicsbench_palisade_amd as g  # noqa: E402
+if os.environ.get("PHMM_LIB"):  # another build of libgb.so, to time two builds on one box
+    g.LIBGB = os.path.abspath(os.environ["PHMM_LIB"])
 from genomicsbench_palisade_amd import gen, phmm, set_device, shard  # noqa: E402
 from genomicsbench_palisade_amd._tc import TestcaseArray  # noqa: E402
 
