@@ -1746,6 +1746,11 @@ def main():
     elif args.gpus > 1 or args.launch_dry_run:
         raise SystemExit(launch(args.gpus, sys.argv[1:], dry_run=args.launch_dry_run))
 
+    # stdout carries exactly one line, the headline: everything else this process prints -- library
+    # banners, torch.distributed's gloo connection messages under a launcher -- goes to stderr
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     world, rank, local = dist_env()
     D = Dist(world)
     import genomicsbench_palisade_amd as gb
@@ -1820,7 +1825,8 @@ def main():
             with open(d, "w") as f:
                 json.dump(line, f)
             log(f"full bench record: {detail} ({len(json.dumps(line))} bytes)")
-        print(json.dumps(headline(line, detail)), flush=True)
+        sys.stdout.flush()
+        os.write(out_fd, (json.dumps(headline(line, detail)) + "\n").encode())
     D.close()
 
 

@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 from genomicsbench_palisade_amd import shard
@@ -96,3 +97,20 @@ def test_smem_keys_follow_the_batches():
     fk = shard.smem_keys(np.zeros(14), full_bc, 0)
     part = shard.smem_keys(np.zeros(7), full_bc[2:], 2)
     assert (fk[7:] == part).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", ["1", "2"])
+def test_stdout_is_one_json_line(gpus, tmp_path):
+    """The driver reads one JSON line from stdout: at N=1 and under the self-launcher at N=2 (two
+    ranks sharing the GPU, gloo connection messages and library banners included) nothing else may
+    reach it."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", gpus, "--only", "phmm", "--batches", "8", "--no-small",
+                        "--no-e2e", "--no-cpu-baseline", "--steps", "2", "--warmup", "1", "--shard-of", "0",
+                        "--detail-out", str(tmp_path / "d.json")],
+                       capture_output=True, text=True, timeout=280, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1, lines[:3]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == int(gpus) and line["value"] > 0
