@@ -959,8 +959,6 @@ int gb_phmm_init(void) {
 
 namespace {
 
-// Pack the testcases (deduplicated reads/haplotypes, LPT order) and upload them into b, growing its
-// device buffers when they are too small. b's stream/events exist already.
 // GB_PHMM_HOSTPROF=1: host phase times of the drop-in path on stderr (development aid)
 struct HostClock {
   bool on;
@@ -1066,7 +1064,9 @@ struct StageLayout {
   }
 };
 
-// threads: host threads of the pack and merge phases (0: up to 8 for jobs of 64 K testcases and more)
+// Pack the testcases (deduplicated reads/haplotypes, stacks in LPT order) into b's pinned staging
+// buffer and upload them, growing its buffers when they are too small; b's stream/events exist
+// already. threads: host threads of the pack and merge phases (0: up to 8 from pack_min testcases).
 int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0) {
   HostClock clk;
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
