@@ -59,8 +59,21 @@ struct TaskArgs {
   int16_t *next_pos;           // per task (OnePos)
   int32_t *rounds;             // per task (AllPos)
   TEnt *prev;                  // per task: maxlen + 2 entries
-  unsigned long long *calls;   // backwardExt calls (work counter)
+  uint32_t *tcalls;            // per task: backwardExt calls (work counter)
+  // the records of every task that fits its slot, packed: task t's at compact[toff[t]], in any task
+  // order (one atomic per task on *cursor), so the host copies back only what was emitted
+  TSmem *compact;
+  int32_t *toff;
+  unsigned long long *cursor;
 };
+
+// a task's records from its slot to the packed array (by the thread that wrote them)
+__device__ __forceinline__ void pack_task(const TaskArgs &A, int t, int cnt) {
+  const int c = cnt > A.cap ? 0 : cnt;  // an overflowing task is re-run with a bigger slot
+  const int32_t off = (int32_t)atomicAdd(A.cursor, (unsigned long long)c);
+  A.toff[t] = off;
+  for (int k = 0; k < c; k++) A.compact[off + k] = A.out[(size_t)t * A.cap + k];
+}
 
 __device__ __forceinline__ void emit(const TaskArgs &A, int t, int &cnt, uint32_t rid, const TEnt &e, uint32_t round) {
   if (cnt < A.cap) {
@@ -302,10 +315,9 @@ __global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
       right_smems(A, t, rid, cnt, calls);
     }
     A.counts[t] = cnt;
+    A.tcalls[t] = calls;
+    pack_task(A, t, cnt);
   }
-  // one atomic per wave for the work counter
-  for (int off = 32; off > 0; off >>= 1) calls += __shfl_down(calls, off, 64);
-  if ((threadIdx.x & 63) == 0 && calls) atomicAdd(A.calls, (unsigned long long)calls);
 }
 
 // The same tasks, one wave per task (fmi_wave.h): a call of a few hundred tasks is latency-bound --
@@ -314,10 +326,19 @@ __global__ __launch_bounds__(64) void fmi_task_kernel(TaskArgs A) {
 // fmi_task_kernel. Reads up to kWaveMaxLen bases (the `prev` lists live in LDS).
 constexpr int kWaveMaxLen = 256;
 
+// LDS: the read, then (OnePos / AllPos) two `prev` lists of maxlen + 1 entries, sized per launch
+// (wave_lds): 151-base reads take 5 KB instead of the 8.5 KB of 256-base lists, so LDS no longer caps
+// the waves per CU below what the registers allow.
+__host__ __device__ inline size_t wave_lds(int mode, int maxlen) {
+  const size_t q = ((size_t)maxlen + 15) & ~(size_t)15;
+  return mode == kLast ? q : q + 2 * sizeof(PEnt) * ((size_t)maxlen + 1);
+}
+
 template <int kMode>
 __global__ __launch_bounds__(64) void fmi_task_wave(TaskArgs A) {
-  __shared__ PEnt La[kWaveMaxLen + 1], Lb[kWaveMaxLen + 1];
-  __shared__ uint8_t Q[kWaveMaxLen];
+  extern __shared__ uint8_t lds[];
+  uint8_t *Q = lds;
+  PEnt *La = reinterpret_cast<PEnt *>(lds + (((size_t)A.maxlen + 15) & ~(size_t)15)), *Lb = La + A.maxlen + 1;
   const int lane = threadIdx.x;
   for (int t = blockIdx.x; t < A.ntasks; t += gridDim.x) {
     const uint32_t rid = (uint32_t)A.rid[t];
@@ -353,25 +374,29 @@ __global__ __launch_bounds__(64) void fmi_task_wave(TaskArgs A) {
     }
     if (lane == 0) {
       A.counts[t] = cnt;
-      if (calls) atomicAdd(A.calls, (unsigned long long)calls);
+      A.tcalls[t] = calls;
+      pack_task(A, t, cnt);
     }
     __syncthreads();
   }
 }
 
-// Per host thread and device: stream and grow-only device buffers (the reference's methods are
-// called from OpenMP threads sharing one FMI_search object).
+// Per host thread and device: stream, grow-only device buffers and a pinned staging buffer (the
+// reference's methods are called from OpenMP threads sharing one FMI_search object).
 struct Workspace {
   int device = -1;
   hipStream_t stream = nullptr;
   void *buf[10] = {nullptr};
   size_t cap[10] = {0};
+  uint8_t *h = nullptr;  // pinned: uploads are packed here, downloads land here
+  size_t hcap = 0;
   ~Workspace() {
     if (device < 0) return;
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     for (void *p : buf) (void)hipFree(p);
+    if (h) (void)hipHostFree(h);
     if (stream) (void)hipStreamDestroy(stream);
     (void)hipSetDevice(cur);
   }
@@ -383,6 +408,16 @@ struct Workspace {
     cap[slot] = 0;
     hipError_t e = hipMalloc(&buf[slot], bytes + bytes / 2);
     if (e == hipSuccess) cap[slot] = bytes + bytes / 2;
+    return e;
+  }
+  hipError_t ensure_host(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 1 << 20);
+    if (hcap >= bytes) return hipSuccess;
+    if (h) (void)hipHostFree(h);
+    h = nullptr;
+    hcap = 0;
+    hipError_t e = hipHostMalloc((void **)&h, bytes + bytes / 2, hipHostMallocDefault);
+    if (e == hipSuccess) hcap = bytes + bytes / 2;
     return e;
   }
 };
@@ -402,8 +437,34 @@ struct HostTasks {
   std::vector<int16_t> qpos;
 };
 
+inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// The checks of one call's tasks (the reads they name, their lengths and query positions); the
+// extent of enc_qdb they read and their longest read.
+int check_tasks(int mode, const int32_t *lens, const int32_t *offs, int32_t nrid, const HostTasks &T,
+                int64_t *extent, int32_t *maxlen) {
+  const int32_t ntasks = (int32_t)T.rid.size();
+  *extent = 0;
+  *maxlen = 1;
+  for (int32_t t = 0; t < ntasks; t++) {
+    const int32_t r = T.rid[t];
+    GB_ARG(r >= 0 && r < nrid, "FMI_search: task %d names read %d outside [0, %d)", t, r, nrid);
+    GB_ARG(lens[r] >= 0 && (lens[r] < 32768 || mode == kRight) && offs[r] >= 0, "FMI_search: read %d has length %d / offset %d", r,
+           lens[r], offs[r]);
+    if (mode == kOnePos)
+      GB_ARG(T.qpos[t] >= 0 && T.qpos[t] < lens[r], "FMI_search: query position %d outside read %d (length %d)",
+             T.qpos[t], r, lens[r]);
+    *extent = std::max<int64_t>(*extent, (int64_t)offs[r] + lens[r]);
+    *maxlen = std::max(*maxlen, lens[r]);
+  }
+  return GB_OK;
+}
+
 // Runs `mode` over the given tasks; fills per-task record lists (reference emission order within a
-// task) and per-task next_pos / rounds. Overflowing tasks are re-run with a larger slot.
+// task) and per-task next_pos / rounds, and counts backwardExt calls. Overflowing tasks are re-run
+// with a larger slot. Per launch: one upload of the task inputs from pinned staging, the kernel
+// (which packs the records of the tasks that fit), one download of the per-task control words and
+// the packed count, one download of the packed records.
 int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *lens, const int32_t *offs, int32_t nrid,
               const HostTasks &T, int32_t min_seed_len, std::vector<std::vector<TSmem>> &recs,
               std::vector<int16_t> *next_pos, std::vector<int32_t> *rounds, int64_t *calls_out) {
@@ -417,24 +478,14 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   if (rounds) rounds->assign(ntasks, 0);
   if (calls_out) *calls_out = 0;
   if (ntasks == 0) return GB_OK;
-  // extent of enc_qdb the tasks read, and the longest read (prev scratch rows)
   int64_t extent = 0;
   int32_t maxlen = 1;
-  for (int32_t t = 0; t < ntasks; t++) {
-    const int32_t r = T.rid[t];
-    GB_ARG(r >= 0 && r < nrid, "FMI_search: task %d names read %d outside [0, %d)", t, r, nrid);
-    GB_ARG(lens[r] >= 0 && (lens[r] < 32768 || mode == kRight) && offs[r] >= 0, "FMI_search: read %d has length %d / offset %d", r,
-           lens[r], offs[r]);
-    if (mode == kOnePos)
-      GB_ARG(T.qpos[t] >= 0 && T.qpos[t] < lens[r], "FMI_search: query position %d outside read %d (length %d)",
-             T.qpos[t], r, lens[r]);
-    extent = std::max<int64_t>(extent, (int64_t)offs[r] + lens[r]);
-    maxlen = std::max(maxlen, lens[r]);
-  }
+  if (int st = check_tasks(mode, lens, offs, nrid, T, &extent, &maxlen)) return st;
   GB_HIP(hipSetDevice(idx->device));
   Workspace &W = workspace(idx->device);
   if (!W.stream) GB_HIP(hipStreamCreateWithFlags(&W.stream, hipStreamNonBlocking));
   if (int st = ensure_occ32(idx, W.stream)) return st;
+  hipStream_t s = W.stream;
 
   TaskArgs A;
   A.F.occ = idx->d_occ32;
@@ -442,6 +493,22 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   A.F.sentinel = idx->sentinel;
   A.min_seed_len = min_seed_len;
   A.maxlen = maxlen;
+
+  // the reads, once per call: [qdb extent | lens | offs]
+  {
+    const size_t o_lens = up256((size_t)extent), o_offs = o_lens + up256(4 * (size_t)nrid),
+                 bytes = o_offs + 4 * (size_t)nrid;
+    GB_HIP(W.ensure(0, bytes));
+    GB_HIP(W.ensure_host(bytes));
+    std::memcpy(W.h, qdb, (size_t)extent);
+    std::memcpy(W.h + o_lens, lens, 4 * (size_t)nrid);
+    std::memcpy(W.h + o_offs, offs, 4 * (size_t)nrid);
+    GB_HIP(hipMemcpyAsync(W.buf[0], W.h, bytes, hipMemcpyHostToDevice, s));
+    A.qdb = (const uint8_t *)W.buf[0];
+    A.lens = (const int32_t *)((uint8_t *)W.buf[0] + o_lens);
+    A.offs = (const int32_t *)((uint8_t *)W.buf[0] + o_offs);
+    GB_HIP(hipStreamSynchronize(s));  // W.h is reused below
+  }
 
   // Tiles of at most ~256 MB of `prev` scratch ((maxlen + 1) entries per task): the per-thread
   // workspace stays bounded whatever the batch. Per tile: the whole tile, then its overflowing
@@ -451,7 +518,6 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   int64_t tile = std::max<int64_t>(1, (256ll << 20) / ((int64_t)(maxlen + 2) * (int64_t)sizeof(TEnt)));
   if (tile >= 64) tile &= ~63ll;
   if (const char *te = getenv("GB_FMI_TASK_TILE")) tile = std::max(1, atoi(te));  // tests: force many tiles
-  bool uploaded = false;
   int64_t calls_sum = 0;
   for (int32_t t0 = 0; t0 < ntasks; t0 = (int32_t)std::min<int64_t>(ntasks, t0 + tile)) {
   const int32_t t1 = (int32_t)std::min<int64_t>(ntasks, t0 + tile);
@@ -460,59 +526,58 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
   int32_t cap = mode == kLast ? 48 : mode == kRight ? 64 : 32;
   for (int pass = 0; pass < 2 && !todo.empty(); pass++) {
     const int32_t n = (int32_t)todo.size();
-    std::vector<int32_t> rid(n), intv(n);
-    std::vector<int16_t> qpos(n);
-    for (int32_t i = 0; i < n; i++) {
-      rid[i] = T.rid[todo[i]];
-      intv[i] = T.intv[todo[i]];
-      qpos[i] = mode == kOnePos ? T.qpos[todo[i]] : 0;
-    }
-    hipError_t e = W.ensure(0, (size_t)extent);
-    if (e == hipSuccess) e = W.ensure(1, sizeof(int32_t) * (size_t)nrid);
-    if (e == hipSuccess) e = W.ensure(2, sizeof(int32_t) * (size_t)nrid);
-    if (e == hipSuccess) e = W.ensure(3, sizeof(int32_t) * (size_t)n);
-    if (e == hipSuccess) e = W.ensure(4, sizeof(int16_t) * (size_t)n);
-    if (e == hipSuccess) e = W.ensure(5, sizeof(int32_t) * (size_t)n);
-    if (e == hipSuccess) e = W.ensure(6, sizeof(TSmem) * (size_t)n * cap);
-    if (e == hipSuccess) e = W.ensure(7, sizeof(int32_t) * 2 * (size_t)n + sizeof(int16_t) * (size_t)n + 64);
+    // task inputs (uploaded): [cursor 8 B | rid n | intv n | qpos n]
+    const size_t i_rid = 256, i_intv = i_rid + up256(4 * (size_t)n), i_qpos = i_intv + up256(4 * (size_t)n),
+                 in_bytes = i_qpos + 2 * (size_t)n;
+    // control words (downloaded): [counts n | rounds n | tcalls n | toff n | next_pos n]
+    const size_t c_rounds = up256(4 * (size_t)n), c_tcalls = c_rounds + up256(4 * (size_t)n),
+                 c_toff = c_tcalls + up256(4 * (size_t)n), c_np = c_toff + up256(4 * (size_t)n),
+                 ctl_bytes = c_np + 2 * (size_t)n;
+    const size_t rec_bytes = sizeof(TSmem) * (size_t)n * cap;
+    hipError_t e = W.ensure(3, in_bytes);
+    if (e == hipSuccess) e = W.ensure(6, rec_bytes);
+    if (e == hipSuccess) e = W.ensure(7, ctl_bytes);
     if (e == hipSuccess) e = W.ensure(8, sizeof(TEnt) * (size_t)n * (maxlen + 2));
-    if (e == hipSuccess) e = W.ensure(9, sizeof(unsigned long long));
+    if (e == hipSuccess) e = W.ensure(9, rec_bytes);
+    if (e == hipSuccess) e = W.ensure_host(std::max(std::max(in_bytes, up256(ctl_bytes) + 256), rec_bytes));
     GB_HIP(e);
-    A.qdb = (const uint8_t *)W.buf[0];
-    A.lens = (const int32_t *)W.buf[1];
-    A.offs = (const int32_t *)W.buf[2];
-    A.rid = (const int32_t *)W.buf[3];
-    A.qpos = (const int16_t *)W.buf[4];
-    A.intv = (const int32_t *)W.buf[5];
+    uint8_t *h = W.h;
+    std::memset(h, 0, 8);
+    auto *hrid = reinterpret_cast<int32_t *>(h + i_rid);
+    auto *hintv = reinterpret_cast<int32_t *>(h + i_intv);
+    auto *hqpos = reinterpret_cast<int16_t *>(h + i_qpos);
+    for (int32_t i = 0; i < n; i++) {
+      hrid[i] = T.rid[todo[i]];
+      hintv[i] = T.intv[todo[i]];
+      hqpos[i] = mode == kOnePos ? T.qpos[todo[i]] : 0;
+    }
+    uint8_t *din = (uint8_t *)W.buf[3], *dctl = (uint8_t *)W.buf[7];
+    GB_HIP(hipMemcpyAsync(din, h, in_bytes, hipMemcpyHostToDevice, s));
+    A.cursor = (unsigned long long *)din;
+    A.rid = (const int32_t *)(din + i_rid);
+    A.intv = (const int32_t *)(din + i_intv);
+    A.qpos = (const int16_t *)(din + i_qpos);
     A.out = (TSmem *)W.buf[6];
-    A.counts = (int32_t *)W.buf[7];
-    A.rounds = A.counts + n;
-    A.next_pos = (int16_t *)(A.rounds + n);
+    A.compact = (TSmem *)W.buf[9];
+    A.counts = (int32_t *)dctl;
+    A.rounds = (int32_t *)(dctl + c_rounds);
+    A.tcalls = (uint32_t *)(dctl + c_tcalls);
+    A.toff = (int32_t *)(dctl + c_toff);
+    A.next_pos = (int16_t *)(dctl + c_np);
     A.prev = (TEnt *)W.buf[8];
-    A.calls = (unsigned long long *)W.buf[9];
     A.ntasks = n;
     A.cap = cap;
-    hipStream_t s = W.stream;
-    if (!uploaded) {
-      GB_HIP(hipMemcpyAsync(W.buf[0], qdb, (size_t)extent, hipMemcpyHostToDevice, s));
-      GB_HIP(hipMemcpyAsync(W.buf[1], lens, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
-      GB_HIP(hipMemcpyAsync(W.buf[2], offs, sizeof(int32_t) * nrid, hipMemcpyHostToDevice, s));
-      uploaded = true;  // buffers 0-2 keep their size (and contents) for the later tiles
-    }
-    if (pass == 0) GB_HIP(hipMemsetAsync(W.buf[9], 0, sizeof(unsigned long long), s));
-    GB_HIP(hipMemcpyAsync(W.buf[3], rid.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    GB_HIP(hipMemcpyAsync(W.buf[4], qpos.data(), sizeof(int16_t) * n, hipMemcpyHostToDevice, s));
-    GB_HIP(hipMemcpyAsync(W.buf[5], intv.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
     // a wave per task when the reads fit its LDS lists (GB_FMI_TASK_WAVE=0: a lane per task)
     const char *we = getenv("GB_FMI_TASK_WAVE");
     if (mode != kRight && maxlen <= kWaveMaxLen && !(we && *we == '0')) {
       const dim3 grid((unsigned)std::min<int64_t>(n, 65535)), block(64);
+      const size_t lds = wave_lds(mode, maxlen);
       if (mode == kOnePos)
-        hipLaunchKernelGGL(fmi_task_wave<kOnePos>, grid, block, 0, s, A);
+        hipLaunchKernelGGL(fmi_task_wave<kOnePos>, grid, block, lds, s, A);
       else if (mode == kAllPos)
-        hipLaunchKernelGGL(fmi_task_wave<kAllPos>, grid, block, 0, s, A);
+        hipLaunchKernelGGL(fmi_task_wave<kAllPos>, grid, block, lds, s, A);
       else
-        hipLaunchKernelGGL(fmi_task_wave<kLast>, grid, block, 0, s, A);
+        hipLaunchKernelGGL(fmi_task_wave<kLast>, grid, block, lds, s, A);
     } else {
       const dim3 grid((unsigned)((n + 63) / 64)), block(64);
       if (mode == kOnePos)
@@ -525,28 +590,40 @@ int run_tasks(gb_fmi_index *idx, int mode, const uint8_t *qdb, const int32_t *le
         hipLaunchKernelGGL(fmi_task_kernel<kRight>, grid, block, 0, s, A);
     }
     GB_HIP(hipGetLastError());
-    std::vector<int32_t> ctl(2 * (size_t)n);
-    std::vector<int16_t> np(n);
-    std::vector<TSmem> out((size_t)n * cap);
-    GB_HIP(hipMemcpyAsync(ctl.data(), A.counts, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, s));
-    GB_HIP(hipMemcpyAsync(np.data(), A.next_pos, sizeof(int16_t) * n, hipMemcpyDeviceToHost, s));
-    GB_HIP(hipMemcpyAsync(out.data(), A.out, sizeof(TSmem) * (size_t)n * cap, hipMemcpyDeviceToHost, s));
-    unsigned long long calls = 0;
-    if (pass == 0) GB_HIP(hipMemcpyAsync(&calls, A.calls, sizeof(calls), hipMemcpyDeviceToHost, s));
+    // the control words and the packed count (the input block's first word) in one download each
+    GB_HIP(hipMemcpyAsync(h, dctl, ctl_bytes, hipMemcpyDeviceToHost, s));
+    unsigned long long packed = 0;
+    GB_HIP(hipMemcpyAsync(h + up256(ctl_bytes), din, 8, hipMemcpyDeviceToHost, s));
     GB_HIP(hipStreamSynchronize(s));
-    if (pass == 0) calls_sum += (int64_t)calls;
+    std::memcpy(&packed, h + up256(ctl_bytes), 8);
+    GB_ARG(packed <= (unsigned long long)n * cap, "FMI_search: %llu packed records exceed the %lld slots", packed,
+           (long long)n * cap);
+    const int32_t *hc = reinterpret_cast<const int32_t *>(h);
+    const std::vector<int32_t> cnt(hc, hc + n), rnd(reinterpret_cast<const int32_t *>(h + c_rounds),
+                                                    reinterpret_cast<const int32_t *>(h + c_rounds) + n),
+        toff(reinterpret_cast<const int32_t *>(h + c_toff), reinterpret_cast<const int32_t *>(h + c_toff) + n);
+    const std::vector<uint32_t> tc(reinterpret_cast<const uint32_t *>(h + c_tcalls),
+                                   reinterpret_cast<const uint32_t *>(h + c_tcalls) + n);
+    const std::vector<int16_t> np(reinterpret_cast<const int16_t *>(h + c_np),
+                                  reinterpret_cast<const int16_t *>(h + c_np) + n);
+    if (packed) {
+      GB_HIP(hipMemcpyAsync(h, A.compact, sizeof(TSmem) * (size_t)packed, hipMemcpyDeviceToHost, s));
+      GB_HIP(hipStreamSynchronize(s));
+    }
+    const TSmem *rec = reinterpret_cast<const TSmem *>(h);
     std::vector<int32_t> again;
     int32_t need = 0;
     for (int32_t i = 0; i < n; i++) {
-      const int32_t t = todo[i], c = ctl[i];
+      const int32_t t = todo[i], c = cnt[i];
+      if (pass == 0) calls_sum += tc[i];
       if (c > cap) {
         again.push_back(t);
         need = std::max(need, c);
         continue;
       }
-      recs[t].assign(out.begin() + (size_t)i * cap, out.begin() + (size_t)i * cap + c);
+      recs[t].assign(rec + toff[i], rec + toff[i] + c);
       if (next_pos) (*next_pos)[t] = np[i];
-      if (rounds) (*rounds)[t] = ctl[n + i];
+      if (rounds) (*rounds)[t] = rnd[i];
     }
     todo.swap(again);
     cap = need;
