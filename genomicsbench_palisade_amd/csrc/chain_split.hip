@@ -640,6 +640,19 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
   const int64_t total = B->ncalls ? offsets[B->ncalls] : 0;
   const char *te = getenv("GB_CHAIN_TARGET");
   const int32_t target = te ? std::max(0, atoi(te)) : (total < (1 << 20) ? 600 : 0);
+  // Under a row target the block is warm-up + capped window (<= 512) + segment, so the window cap
+  // bounds it from below; a shorter segment floor and warm-up take it under: the 'small' 1/8 shard
+  // 0.678 -> 0.637 ms at a 64-anchor floor and a 16-anchor warm-up, no failed guess on the bench's or
+  // the tests' sets (profiles/r05zz8_chain_knobs.log; a failed guess costs a fix-up, never a result).
+  // GB_CHAIN_SEGMIN sets the floor; GB_CHAIN_SPLIT's warm-up, when given, wins.
+  const char *sm = getenv("GB_CHAIN_SEGMIN");
+  const int32_t seg_floor = sm ? std::max(16, atoi(sm)) : 64;
+  {
+    const char *se = getenv("GB_CHAIN_SPLIT");
+    int a = 0, b = -1;
+    const bool warm_given = se && sscanf(se, "%d,%d", &a, &b) >= 2 && b >= 0;
+    if (target > 0 && !warm_given) warm = std::min(warm, 16);
+  }
   const int64_t ncalls = B->ncalls;
   B->vc.clear();
   B->split.clear();
@@ -712,7 +725,7 @@ int split_plan(gb_chain_batch *B, const int64_t *offsets, const uint64_t *x, con
               continue;
             }
             const int32_t cw = std::min(maxwin[(size_t)c], wcap);
-            segc = std::max(128, std::min(seg, target - cw - warm));
+            segc = std::max(seg_floor, std::min(seg, target - cw - warm));
           }
           // equal segments of at most segc anchors: the longest block of the launch (a segment, its
           // window and its warm-up) is then bounded by segc, not by a last segment of up to 2 segc - 1

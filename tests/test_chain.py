@@ -258,14 +258,18 @@ def test_gpu_rows_long_windows(monkeypatch, split):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("target", ["600", "300", "0"])
-def test_gpu_split_row_target(target, monkeypatch):
+@pytest.mark.parametrize("target,segmin,fault", [("600", "", 0), ("300", "", 0), ("0", "", 0), ("600", "16", 37)])
+def test_gpu_split_row_target(target, segmin, fault, monkeypatch):
     """Per-call segment lengths under a row target (GB_CHAIN_TARGET; a batch under 1 M anchors takes
-    600 by default): calls longer than the target split into segments as long as their window leaves
-    room for, shorter ones run whole -- bit-exact against the oracle either way."""
+    600 by default, with segments of >= 64 anchors and a 16-anchor warm-up): calls longer than the
+    target split into segments as long as their window leaves room for, shorter ones run whole --
+    bit-exact against the oracle either way, also with 16-anchor segments and injected wrong guesses."""
     from genomicsbench_palisade_amd import chain, set_device
     set_device(0)
     monkeypatch.setenv("GB_CHAIN_TARGET", target)
+    if segmin:
+        monkeypatch.setenv("GB_CHAIN_SEGMIN", segmin)
+    monkeypatch.setenv("GB_CHAIN_SPLIT_FAULT", str(fault))
     calls = gen.chain_dataset("small", num_calls=300, seed=31, median_n=1500, max_n=30000)
     exp = oracle_lib.chain_oracle(calls, 8)
     b = chain.ChainBatch(calls)
@@ -274,5 +278,8 @@ def test_gpu_split_row_target(target, monkeypatch):
     assert_same(got, exp)
     assert got[4] == exp[4]
     if target != "0":
-        assert b.split_stats()[0] > 0
+        ns, rounds, fixups = b.split_stats()
+        assert ns > 0
+        if fault:
+            assert fixups > 0 and rounds > 1
     b.close()

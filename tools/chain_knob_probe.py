@@ -25,7 +25,7 @@ if os.environ.get("CHAIN_SETS"):
     sets = [s for s in sets if s[0] in os.environ["CHAIN_SETS"].split(",")]
 configs = os.environ.get("CHAIN_CONFIGS", "").split(";")
 KNOBS = ("GB_CHAIN_SPLIT", "GB_CHAIN_ROWS", "GB_CHAIN_ROWS_MAXN", "GB_CHAIN_VLANES", "GB_CHAIN_PRIO", "GB_CHAIN_SPREAD",
-         "GB_CHAIN_EXP", "GB_CHAIN_TARGET")
+         "GB_CHAIN_EXP", "GB_CHAIN_TARGET", "GB_CHAIN_SEGMIN")
 
 
 def parse_cfg(cfg):
