@@ -433,7 +433,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NCH >= 16 ? 
         const int y = (int)(x >> 16) + sb;                                    // H + S
         const int M = med3_0((int)(x & 0xFFFF0000u), y);  // H ? H + S : 0 (clamped); H << 16 >= 0 (H < 2^15)
         const int e = (int)(x & 0xFFFFu);
-        const int h = max(max(M, e), f);
+        // one max3 (asm: the compiler folds the mask into an SDWA max and then needs a second max,
+        // two 4.2-cycle ops where the AND is a 2.5-cycle one)
+        int h;
+        asm("v_max3_i32 %0, %1, %2, %3" : "=v"(h) : "v"(M), "v"(e), "v"(f));
         const int en = max(max(e - e_del, M - oe_del), 0);                    // E(i+1,j)
         const int fn = max(max(f - e_ins, M - oe_ins), 0);                    // F(i,j+1)
         // eh[j] = {H(i,j-1), E}: h1 written into the high word of en's register (an SDWA move issues at
