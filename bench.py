@@ -248,11 +248,14 @@ def cpu_baseline_phmm(ta, sample_seconds: float, gpu=None, threads=None):
            "sample": f"{m} of {ta.n} testcases ({sub.cells() / 1e9:.2f} G cells, random) of the same "
                      f"job x {reps} passes, {eng} GKL kernels, OpenMP {threads} threads, {t:.1f} s"}
     if gpu is not None:
+        from genomicsbench_palisade_amd.phmm import parity_mismatches
         sel = order[:m]
-        bad = {name: int((g[sel].view(u) != e.view(u)).sum())
-               for name, g, e, u in zip(("log10", "raw_f32", "raw_f64"), gpu, last["out"],
-                                        (np.uint64, np.uint32, np.uint64))}
+        # what computelikelihoodsboth exposes, bit for bit: final log10, raw f64, the fallback choice,
+        # raw f32 of the passing testcases (below MIN_ACCEPTED the f32 early exit may leave 0)
+        bad = parity_mismatches(tuple(np.ascontiguousarray(g[sel]) for g in gpu), last["out"])
+        dropped = bad.pop("f32_dropped")
         res["parity_check"] = {"testcases": int(m), "of": int(ta.n), "mismatches": bad,
+                               "f32_early_exit_dropped": dropped,
                                "bit_exact": not any(bad.values()),
                                "against": f"reference GKL {eng}" if ref is not None else "C restatement"}
         if any(bad.values()):
@@ -1149,9 +1152,16 @@ def bench_phmm(args, D, rank, world, kind="large"):
     ms64 = float(np.mean(k64)) if k64 else 0.0
     cells_all = D.sum(float(cells))
     gcups = cells_all * args.steps / elapsed / 1e9
-    r32 = {"bound": "valu", "kernel": "phmm_forward<float>",
-           "achieved": PHMM_FLOP_PER_CELL * cells / (ms32 * 1e-3) / 1e12, "peak": PEAK_F32_OPS / 1e12,
-           "unit": "TFLOP/s (non-FMA FP ops)"}
+    # the f32 pass's early exit drops testcases proven to fall back before their last rows: its
+    # roofline counts the cells it computed (the step's GCUPS counts every cell of the job, as the
+    # reference's does)
+    dropped, skipped = job.exit_stats()
+    cells32 = cells - skipped
+    r32 = {"bound": "valu", "kernel": "phmm_forward<float> (with the f32 early exit)",
+           "achieved": PHMM_FLOP_PER_CELL * cells32 / (ms32 * 1e-3) / 1e12, "peak": PEAK_F32_OPS / 1e12,
+           "unit": "TFLOP/s (non-FMA FP ops)", "cells": cells32,
+           "early_exit": {"testcases_dropped": dropped, "cells_skipped": skipped,
+                          "cells_skipped_frac": skipped / max(cells, 1)}}
     r32["frac"] = r32["achieved"] / r32["peak"]
     r64 = {"bound": "valu", "kernel": "phmm_forward<double> (f64 fallback, its testcases only)",
            "achieved": PHMM_FLOP_PER_CELL * cells_f64 / max(ms64 * 1e-3, 1e-12) / 1e12, "peak": PEAK_F64_OPS / 1e12,
@@ -1164,8 +1174,9 @@ def bench_phmm(args, D, rank, world, kind="large"):
                   if args.scaling == "strong" and world > 1 else shard_note(args, "testcases", 0, full.n, full.n, world)),
         "roofline": r32, "roofline_f64": r64,
         "kernels_ms": {"phmm_forward<float>": ms32, "phmm_forward<double>": ms64},
-        # the f32 pass alone over every cell: what the step would be without the f64 fallback (its
-        # 36 % share of testcases is a property of the synthetic generator)
+        # the job's cells over the f32 pass alone (the early exit skips part of the fallback
+        # testcases' rows): what the step would be without the f64 fallback (its 36 % share of
+        # testcases is a property of the synthetic generator)
         "f32_only_gcups": cells / max(ms32 * 1e-3, 1e-12) / 1e9,
     }
     if world > 1:

@@ -42,12 +42,14 @@ def _declare(L):
     L.gb_phmm_init.argtypes = []
     L.gb_phmm_compute.argtypes = [vp, ci, vp, vp, vp, vp]
     L.gb_phmm_compute_f64.argtypes = [vp, ci, vp]
+    L.gb_phmm_compute_f32.argtypes = [vp, ci, vp]
     L.gb_phmm_batch_create.argtypes = [vp, ci, ctypes.POINTER(vp)]
     L.gb_phmm_batch_run.argtypes = [vp]
     L.gb_phmm_batch_sync.argtypes = [vp]
     L.gb_phmm_batch_results.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gb_phmm_batch_timing.argtypes = [vp, fp, fp, fp]
     L.gb_phmm_batch_stats.argtypes = [vp, i64p, i64p, i64p]
+    L.gb_phmm_batch_exit_stats.argtypes = [vp, i64p, i64p]
     L.gb_phmm_batch_destroy.argtypes = [vp]
 
 

@@ -51,10 +51,8 @@ void computelikelihoodsfloat(testcase *testcases, float *expected_result) {
   ensure_device();
   // f32 probability only (no f64 fallback), as IntelPairHmmCSource.cpp:89-99
   float rf = 0.f;
-  double res = 0.0;
-  int st = gb_phmm_compute(reinterpret_cast<const gb_testcase *>(testcases), 1, &res, &rf, nullptr,
-                           nullptr);
-  if (st) die("gb_phmm_compute", st);
+  int st = gb_phmm_compute_f32(reinterpret_cast<const gb_testcase *>(testcases), 1, &rf);
+  if (st) die("gb_phmm_compute_f32", st);
   *expected_result = (float)(double)(log10f(rf) - log10f(ldexpf(1.f, 120)));
 }
 

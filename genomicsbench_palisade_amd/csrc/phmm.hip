@@ -368,13 +368,13 @@ __device__ __forceinline__ int scan_add(int v) {  // wave-wide inclusive prefix 
   return v;
 }
 
-// One stack. f32 pass: every testcase; f64 pass: those whose f32 result is below MIN_ACCEPTED
-// (all of them when `force`). Returns the number of testcases computed.
-template <typename T, bool kF64Pass>
+// One stack. f32 pass: every testcase (kExit: with the early exit below); f64 pass: those whose f32
+// result is below MIN_ACCEPTED (all of them when `force`). Returns the number of testcases computed.
+template <typename T, bool kF64Pass, bool kExit = false>
 __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
                           const uint8_t *__restrict__ pool, const DevTab<T> &tab, T *__restrict__ raw_out,
                           const float *__restrict__ raw_f, bool force, uint8_t *smem_raw, int part = 0,
-                          int parts = 1) {
+                          int parts = 1, unsigned long long *exit_stats = nullptr) {
   const int lane = threadIdx.x;
   const int C = (int)S.C;
   // LDS: boundary records for columns [-kRecPad, C+kBndPad) and the haplotype codes for columns
@@ -421,9 +421,10 @@ __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__rest
     hcol[c] = (c >= 1 && c <= C) ? hcode[c - 1] : (c == 0 ? 5 : (c < 0 ? 6 : 0));
   __syncthreads();
 
-  const int nstripes = (T_rows + kWave - 1) / kWave;
-  for (int s = 0; s < nstripes; s++) {
-    const int g = s * kWave + lane;
+  // the stripe loop walks stacked rows from `base`; an early exit (f32 pass, `force` set) can skip the
+  // rest of a testcase, so the stripes are not at fixed multiples of 64
+  for (int base = 0; base < T_rows;) {
+    const int g = base + lane;
     // the lane's testcase: the last entry starting at or before row g
     int lo = 0, hi = na - 1;
     while (__builtin_amdgcn_ballot_w64(lo < hi)) {  // per-lane binary search over lanes' starts
@@ -485,10 +486,18 @@ __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__rest
     }
     const bool last_row = !dead && r == e.R + 1;
     const uint64_t lastmask = __builtin_amdgcn_ballot_w64(last_row);
-    const bool more = s < nstripes - 1;
-    const int steps = more ? C + kWave - 1 : C + (T_rows - s * kWave) - 1;
+    const bool more = base + kWave < T_rows;
+    const int steps = more ? C + kWave - 1 : C + (T_rows - base) - 1;
     T sumM = (T)0, sumX = (T)0;
     T *out = raw_out + e.out_idx;
+    // lane 63's row and testcase for the early exit below, taken before the sweep into scalars
+    int r63 = 0, R63 = 0, start63 = 0, out63 = 0;
+    if (kExit && more) {
+      r63 = __builtin_amdgcn_readlane(r, 63);
+      R63 = __builtin_amdgcn_readlane(e.R, 63);
+      start63 = __builtin_amdgcn_readlane(e.start, 63);
+      out63 = __builtin_amdgcn_readlane((int)e.out_idx, 63);
+    }
     if (lastmask) {
       if (more)
         phmm_stripe<T, true, true>(steps, st, P, sumM, sumX, bnd, hcol, C, lane, lastmask, out);
@@ -498,6 +507,36 @@ __device__ __forceinline__ int phmm_stack(const Stack &S, const uint32_t *__rest
       phmm_stripe<T, false, true>(steps, st, P, sumM, sumX, bnd, hcol, C, lane, 0, out);
     }
     __syncthreads();
+    int next = base + kWave;
+    if constexpr (!kF64Pass && kExit) {
+      // Early exit (GB_PHMM_EXIT): every path of a testcase crosses from its row r to row r+1 once,
+      // and what follows multiplies by transitions and emissions <= 1, so its result is at most the
+      // crossing mass sum_c (z + w) of row r -- the records lane 63 just wrote for the next stripe,
+      // already multiplied by row r+1's transitions. Below MIN_ACCEPTED / 4 (margin for the f32
+      // rounding of the sum and of the rows not computed) the testcase must fail the f32 test: its
+      // remaining rows are skipped, its f32 result is written as 0, and the f64 pass computes it as
+      // it would have anyway. Only rows with a row of the same testcase below them are tested.
+      if (r63 >= 2 && r63 <= R63) {
+        T acc = (T)0;
+#pragma unroll 1
+        for (int c = 1 + lane; c <= C; c += kWave) acc += bnd[c].z + bnd[c].w;
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        // the sum is the same in every lane; readfirstlane tells the compiler so (a divergent loop
+        // bound would turn the whole stripe loop into per-lane control flow)
+        if (__builtin_amdgcn_readfirstlane(acc < (T)0.25e-28f ? 1 : 0)) {
+          next = start63 + R63 + 2;  // the next testcase's first (virtual) row
+          if (lane == 0) {
+            raw_out[(uint32_t)out63] = (T)0;
+            // exit_stats[0] testcases dropped, [1] their cells not computed (real rows from the next
+            // stripe's first row to the testcase's last)
+            atomicAdd(exit_stats, 1ull);
+            atomicAdd(exit_stats + 1, (unsigned long long)(next - (base + kWave)) * (unsigned long long)C);
+          }
+        }
+        __syncthreads();
+      }
+    }
+    base = next;
   }
   return na;
 }
@@ -753,7 +792,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W ? W : 1, 8
 // `scratch` (scratch_stride bytes per workgroup, global memory: lane 63's record stores and lane 0's
 // loads of the next stripe are ordered by the stripe's __syncthreads), and both passes take the
 // stacks through a persistent grid (counter[2] f32, counter[3] f64).
-template <typename T, bool kF64Pass, bool kLong = false>
+template <typename T, bool kF64Pass, bool kLong = false, bool kExit = false>
 __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ stacks, int nstacks,
                                                     const uint32_t *__restrict__ stk_tc,
                                                     const TcDesc *__restrict__ descs,
@@ -780,7 +819,8 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
     }
     if (kF64Pass && threadIdx.x == 0 && done) atomicAdd(counter, done);
   } else {
-    phmm_stack<T, false>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec);
+    phmm_stack<T, false, kExit>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec, 0, 1,
+                                reinterpret_cast<unsigned long long *>(counter + 4));
   }
 }
 
@@ -857,8 +897,8 @@ int get_device_tables(DeviceTables **out) {
   if (st) return st;
   st = upload_tables(*g_hd, &t->d);
   if (st) return st;
-  for (auto fn : {(const void *)phmm_forward<float, false>, (const void *)phmm_forward<double, true>,
-                  (const void *)phmm_forward2<0>, (const void *)phmm_forward2<6>, (const void *)phmm_forward2<8>})
+  for (auto fn : {(const void *)phmm_forward<float, false>, (const void *)phmm_forward<float, false, false, true>,
+                  (const void *)phmm_forward<double, true>, (const void *)phmm_forward2<0>, (const void *)phmm_forward2<6>, (const void *)phmm_forward2<8>})
     GB_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   g_dev[dev] = t;
   *out = t;
@@ -926,6 +966,7 @@ struct gb_phmm_batch {
   uint8_t *d_scratch = nullptr;    // their boundary records, scratch_stride bytes per workgroup
   size_t scratch_stride = 0, cap_scratch = 0;
   int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter,
+                           // [4..7] the f32 early exit's two u64 counts (testcases, cells skipped),
                            // [2] / [3] the kLong f32 / f64 stack counters
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
@@ -935,6 +976,7 @@ struct gb_phmm_batch {
   int rpl = 1;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=2: two, for A/B probes)
   int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
   int f64_parts = 2;  // work units per stack in the f64 pass (GB_PHMM_F64_PARTS)
+  bool f32_exit = true;  // the f32 pass's early exit (phmm_stack kExit; GB_PHMM_EXIT=0 turns it off)
   // host scratch of the fills (grow-only, host_reserve)
   std::vector<uint32_t> hid;
   std::vector<Stack> stacks;
@@ -1013,7 +1055,7 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
     GB_HIP(hipMalloc(&b->d_pool, pool_bytes));
     b->cap_pool = pool_bytes;
   }
-  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 4 * sizeof(int)));
+  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 8 * sizeof(int)));
   return GB_OK;
 }
 
@@ -1265,6 +1307,11 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
   // unchanged (13.62 -> 13.54 ms); four: no gain (profiles/r05e_phmm_f64_parts.log)
   b->f64_parts = 2;
   if (const char *e = getenv("GB_PHMM_F64_PARTS")) b->f64_parts = std::max(1, std::min(8, atoi(e)));
+  // the f32 pass drops a testcase's remaining rows once its crossing mass proves it falls back to f64
+  // (phmm_stack kExit): f32 pass 19.05 -> 18.40 ms, step +2.0 % (profiles/r05zzi_phmm_exit_ab.log);
+  // finals, raw f64 and the fallback choice unchanged, a dropped testcase's raw f32 reads 0
+  b->f32_exit = true;
+  if (const char *e = getenv("GB_PHMM_EXIT")) b->f32_exit = atoi(e) != 0;
   int stack_rows = kStackRows;
   if (total_rows / stack_rows < 4ll * 32 * b->cus) stack_rows = 1024;
   if (stack_rows == 1024 && total_rows / stack_rows < 16ll * b->cus) stack_rows = 512;
@@ -1415,7 +1462,7 @@ int warm_up(DeviceTables *t) {
     gb_phmm_batch *w = thread_workspace(t, &st, c);
     if (!w) return st;
     if ((st = batch_reserve(w, 1, 16))) return st;
-    GB_HIP(hipMemsetAsync(w->d_count, 0, 4 * sizeof(int), w->stream));
+    GB_HIP(hipMemsetAsync(w->d_count, 0, 8 * sizeof(int), w->stream));
     GB_HIP(hipEventRecord(w->ev[0], w->stream));
   }
   for (int c = 1; c < kPipeMaxChunks; c++) GB_HIP(hipStreamSynchronize(thread_workspace(t, &st, c)->stream));
@@ -1531,7 +1578,7 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipSetDevice(t->device));
   const int n = b->n;
   GB_HIP(hipEventRecord(b->ev[0], b->stream));
-  GB_HIP(hipMemsetAsync(b->d_count, 0, 4 * sizeof(int), b->stream));
+  GB_HIP(hipMemsetAsync(b->d_count, 0, 8 * sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
     const size_t rec = (size_t)(b->max_haplen + kBndPad + kRecPad), codes = (size_t)(b->max_haplen + kBndPad + kWave);
@@ -1541,6 +1588,7 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
     auto f64k = phmm_forward<double, true>;
     const int ns = b->nstacks, nl = b->n_long;
     const Stack *d_long = b->d_stacks + ns;
+    if (b->f32_exit) f32k = phmm_forward<float, false, false, true>;
     if (!b->force_f64) {
       if (ns > 0 && b->rpl == 2) {
         const size_t lds_f2 = sizeof(Brec<float>) * (size_t)(b->max_haplen + kBndPad2 + kRecPad) +
@@ -1676,6 +1724,18 @@ int gb_phmm_batch_stats(gb_phmm_batch *b, int64_t *testcases, int64_t *cells, in
   return GB_OK;
 }
 
+int gb_phmm_batch_exit_stats(gb_phmm_batch *b, int64_t *dropped, int64_t *cells_skipped) {
+  GB_ARG(b, "gb_phmm_batch_exit_stats: null batch");
+  unsigned long long c[2] = {0, 0};
+  if (b->ran) {
+    GB_HIP(hipStreamSynchronize(b->stream));
+    GB_HIP(hipMemcpy(c, b->d_count + 4, sizeof(c), hipMemcpyDeviceToHost));
+  }
+  if (dropped) *dropped = (int64_t)c[0];
+  if (cells_skipped) *cells_skipped = (int64_t)c[1];
+  return GB_OK;
+}
+
 int gb_phmm_batch_destroy(gb_phmm_batch *b) {
   if (!b) return GB_OK;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
@@ -1727,6 +1787,24 @@ int gb_phmm_compute_f64(const gb_testcase *tcs, int n, double *raw_d) {
   st = gb_phmm_batch_run(b);
   b->force_f64 = false;
   if (!st) st = gb_phmm_batch_results(b, nullptr, nullptr, raw_d, nullptr, nullptr);
+  return st;
+}
+
+int gb_phmm_compute_f32(const gb_testcase *tcs, int n, float *raw_f) {
+  gb::Range range_("gb.phmm.compute_f32");
+  GB_ARG(n >= 0 && raw_f && (n == 0 || tcs), "gb_phmm_compute_f32: bad arguments");
+  if (n == 0) return GB_OK;
+  DeviceTables *tabs = nullptr;
+  int st = get_device_tables(&tabs);
+  if (st) return st;
+  gb_phmm_batch *b = thread_workspace(tabs, &st);
+  if (!b) return st;
+  b->force_f64 = false;
+  if ((st = batch_fill(b, tcs, n))) return st;
+  b->f32_exit = false;  // every testcase's f32 probability in full, also those that fall back
+  st = gb_phmm_batch_run(b);
+  if (!st) st = gb_phmm_batch_sync(b);
+  if (!st) st = gb_phmm_batch_results(b, nullptr, raw_f, nullptr, nullptr, nullptr);
   return st;
 }
 

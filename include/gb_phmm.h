@@ -49,12 +49,20 @@ int gb_phmm_init(void);
  *
  * computelikelihoodsboth(): results[k] = log10-likelihood of tcs[k], bit-identical to the
  * reference. raw_f / raw_d / used_double may be NULL; when given they receive the raw f32
- * probability, the raw f64 probability (0 when the f64 pass was not needed) and the fallback flag. */
+ * probability, the raw f64 probability (0 when the f64 pass was not needed) and the fallback flag.
+ * The reference never exposes the raw f32 value of a testcase that falls back (result below
+ * MIN_ACCEPTED = 1e-28f): for those, raw_f holds a value below MIN_ACCEPTED -- the reference's, or 0
+ * when the f32 pass's early exit proved the fallback before the last row (GB_PHMM_EXIT=0 turns the
+ * exit off). raw_f of every testcase that does not fall back is bit-identical to the reference. */
 int gb_phmm_compute(const gb_testcase *tcs, int n, double *results, float *raw_f, double *raw_d,
                     uint8_t *used_double);
 
 /* computelikelihoodsdouble(): raw f64 probability for every testcase (no f32 pass). */
 int gb_phmm_compute_f64(const gb_testcase *tcs, int n, double *raw_d);
+
+/* computelikelihoodsfloat() (IntelPairHmmCSource.cpp:89-99): raw f32 probability of every testcase
+ * in full, also of those below MIN_ACCEPTED (no early exit). */
+int gb_phmm_compute_f32(const gb_testcase *tcs, int n, float *raw_f);
 
 /* Device-resident batches: pack + upload once, run many times (what bench.py times). */
 typedef struct gb_phmm_batch gb_phmm_batch;
@@ -72,6 +80,10 @@ int gb_phmm_batch_results(gb_phmm_batch *b, double *results, float *raw_f, doubl
 int gb_phmm_batch_timing(gb_phmm_batch *b, float *f32_ms, float *f64_ms, float *total_ms);
 /* Batch statistics: testcases, cells = sum(rslen*haplen), f64 fallbacks of the last run. */
 int gb_phmm_batch_stats(gb_phmm_batch *b, int64_t *testcases, int64_t *cells, int64_t *n_f64);
+/* The f32 pass's early exit in the last run: testcases it dropped before their last row (their
+ * raw f32 reads 0; they fall back to f64 as they would have) and the read-row x haplotype cells it
+ * did not compute for them. */
+int gb_phmm_batch_exit_stats(gb_phmm_batch *b, int64_t *dropped, int64_t *cells_skipped);
 int gb_phmm_batch_destroy(gb_phmm_batch *b);
 
 #ifdef __cplusplus

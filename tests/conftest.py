@@ -47,6 +47,21 @@ def bits(a):
     return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
 
 
+def assert_phmm_exact(got, expect):
+    """(results, raw f32, raw f64[, used_double]) of the HIP path against the reference's / the
+    oracle's: bit-exact on everything computelikelihoodsboth exposes (phmm.parity_mismatches: raw f32
+    where the reference's passes MIN_ACCEPTED, the reference's value or the early exit's 0 below it),
+    and the same fallback choice."""
+    from genomicsbench_palisade_amd.phmm import MIN_ACCEPTED, parity_mismatches
+    got = tuple(np.ascontiguousarray(x) for x in got)
+    expect = tuple(np.ascontiguousarray(x) for x in expect)
+    bad = parity_mismatches(got, expect)
+    assert not (bad["log10"] or bad["raw_f32"] or bad["raw_f64"]), bad
+    if len(got) > 3:
+        assert (got[3].astype(bool) == (expect[1] < MIN_ACCEPTED)).all(), "fallback choice differs"
+    return bad
+
+
 def gpu_available():
     try:
         import genomicsbench_palisade_amd as gb

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from conftest import bits
+from conftest import assert_phmm_exact, bits
 from genomicsbench_palisade_amd import gen
 from genomicsbench_palisade_amd._tc import TestcaseArray
 
@@ -86,9 +86,7 @@ def test_phmm_gpu_edges_bit_exact():
     ta = phmm_edge_cases()
     got = phmm.compute_likelihoods_both(ta)
     exp = phmm_oracle(ta)
-    for k, name in enumerate(("log10", "raw f32", "raw f64")):
-        bad = np.nonzero(bits(got[k]) != bits(exp[k]))[0]
-        assert len(bad) == 0, f"{name}: {len(bad)} testcases differ, first {bad[:5]}: {got[k][bad[:3]]} vs {exp[k][bad[:3]]}"
+    assert_phmm_exact(got, exp)
 
 
 @pytest.mark.gpu
@@ -115,8 +113,7 @@ def test_phmm_gpu_longest_haplotype():
     got = phmm.compute_likelihoods_both(ok)
     exp = phmm_oracle(ok)
     assert (exp[1] < 1e-28).any() and (exp[1] >= 1e-28).any()  # both passes exercised
-    for k in range(3):
-        assert (bits(got[k]) == bits(exp[k])).all(), k
+    assert_phmm_exact(got, exp)
     too_long = TestcaseArray.from_pairs([((src[:12].tobytes(),) + qs, (src.tobytes() * 2)[:65536])])
     with pytest.raises(GbError):
         phmm.compute_likelihoods_both(too_long)

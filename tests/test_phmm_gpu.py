@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, bits
+from conftest import ROOT, assert_phmm_exact, bits
 from genomicsbench_palisade_amd import gen
 from genomicsbench_palisade_amd._tc import TestcaseArray
 
@@ -35,13 +35,15 @@ def oracle_run(ta):
 
 
 def assert_exact(got, expect):
-    g_out, g_rf, g_rd = got[:3]
-    e_out, e_rf, e_rd = expect[:3]
-    bad = np.nonzero(bits(g_rf) != bits(e_rf))[0]
-    assert len(bad) == 0, f"raw f32 mismatch at {bad[:10]}: {g_rf[bad[:5]]} vs {e_rf[bad[:5]]}"
-    bad = np.nonzero(bits(g_rd) != bits(e_rd))[0]
-    assert len(bad) == 0, f"raw f64 mismatch at {bad[:10]}: {g_rd[bad[:5]]} vs {e_rd[bad[:5]]}"
-    assert (bits(g_out) == bits(e_out)).all()
+    """Everything computelikelihoodsboth exposes, bit for bit (conftest.assert_phmm_exact)."""
+    return assert_phmm_exact(got, expect)
+
+
+def assert_raw_exact(got, expect):
+    """Raw f32 of every testcase too: the f32 pass without its early exit (GB_PHMM_EXIT=0)."""
+    for k, name in enumerate(("log10", "raw f32", "raw f64")):
+        bad = np.nonzero(bits(got[k]) != bits(expect[k]))[0]
+        assert len(bad) == 0, f"{name} mismatch at {bad[:10]}: {got[k][bad[:5]]} vs {expect[k][bad[:5]]}"
 
 
 @pytest.mark.parametrize("which", ["cross", "pairs"])
@@ -54,6 +56,36 @@ def test_kat(phmm):
     ta = TestcaseArray.from_pairs([((b"ACGT", b"++++", b"++++", b"++++", b"++++"), b"ACGT")])
     res = phmm.compute_likelihoods_both(ta)[0]
     assert res[0] == -0.6022796630859375
+
+
+def test_golden_raw_f32_without_exit(phmm, phmm_golden, monkeypatch):
+    """With the early exit off every raw f32 value is the reference's, also below MIN_ACCEPTED."""
+    monkeypatch.setenv("GB_PHMM_EXIT", "0")
+    for which in ("cross", "pairs"):
+        assert_raw_exact(phmm.compute_likelihoods_both(phmm_golden[which]), phmm_golden[which + "_expect"])
+
+
+def test_compute_f32_full(phmm):
+    """computelikelihoodsfloat's path (gb_phmm_compute_f32): the full raw f32 of every testcase, the
+    ones that fall back included, on a job where the early exit drops some."""
+    rng = np.random.default_rng(41)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 40, 16) for _ in range(3)])
+    exp = oracle_run(ta)
+    assert (exp[1] < 1e-28).sum() > 0
+    assert (bits(phmm.compute_f32(ta)) == bits(exp[1])).all()
+
+
+def test_early_exit_drops_and_stays_exact(phmm, monkeypatch):
+    """The early exit (phmm_stack kExit) drops testcases on a job shaped like the bench's (reads that
+    fall back by far), the outputs computelikelihoodsboth exposes stay bit-exact, and with the exit
+    off the same job reproduces every raw f32 value."""
+    rng = np.random.default_rng(43)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 64, 32) for _ in range(4)])
+    exp = oracle_run(ta)
+    bad = assert_exact(phmm.compute_likelihoods_both(ta), exp)
+    assert bad["f32_dropped"] > 0, bad
+    monkeypatch.setenv("GB_PHMM_EXIT", "0")
+    assert_raw_exact(phmm.compute_likelihoods_both(ta), exp)
 
 
 @pytest.mark.parametrize("seed,kind", [(1, "large"), (2, "small"), (3, "long")])
@@ -173,7 +205,6 @@ def test_stack_edges_vs_oracle(phmm, seed):
     got = phmm.compute_likelihoods_both(ta)
     exp = oracle_run(ta)
     assert_exact(got, exp)
-    assert (got[3].astype(bool) == exp[3].astype(bool)).all()
 
 
 @pytest.mark.parametrize("chunks", ["3", "1", "6"])
@@ -187,7 +218,6 @@ def test_pipelined_compute_bit_exact(phmm, monkeypatch, chunks):
     ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(5)])
     got = phmm.compute_likelihoods_both(ta)
     assert_exact(got, oracle_run(ta))
-    assert (got[3].astype(bool) == (got[1] < np.float32(1e-28))).all()
 
 
 def big_pool_job(seed=31, n=600):
@@ -218,8 +248,7 @@ def test_pipelined_fresh_workspaces_bit_exact(tmp_path):
     z = np.load(out)
     ta = big_pool_job()
     exp = oracle_run(ta)
-    assert_exact((z["out"], z["rf"], z["rd"]), exp)
-    assert (z["ud"].astype(bool) == exp[3].astype(bool)).all()
+    assert_exact((z["out"], z["rf"], z["rd"], z["ud"]), exp)
 
 
 def test_pipelined_big_pool_bit_exact(phmm, monkeypatch):
@@ -234,6 +263,7 @@ def test_rows_per_lane_ab_identical(phmm, monkeypatch):
     on a job with many stacks, partial stripes and both passes."""
     rng = np.random.default_rng(29)
     ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 50, 20) for _ in range(4)])
+    monkeypatch.setenv("GB_PHMM_EXIT", "0")  # the two-row kernel has no early exit: compare every raw f32
     outs = []
     for rpl in ("1", "2"):
         monkeypatch.setenv("GB_PHMM_RPL", rpl)

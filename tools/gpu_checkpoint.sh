@@ -7,8 +7,11 @@
 #   pmcsum those passes summarised into profiles/TAG_pmc.json on the box (run before bench, so the
 #          bench line's traffic is this checkpoint's)
 #   lds    LDS-conflict / VALU-busy SQ counters per leg (tools/gpu_lds.sh)
+#   probe  one probe script per call: PROBE="tools/x.py args" -> gpurun_out/probe_TAG.log
 # Usage: gpu_checkpoint.sh TAG [stages...]   (default stages: tests smoke bench)
 #   gpurun --timeout 1200 -- 'bash tools/gpu_checkpoint.sh r04a tests smoke bench prof'
+# Environment: TESTS (pytest paths / -k, default "tests"), BENCH_ARGS (default "--steps 20 --warmup 5"),
+#   PROBE (the probe stage's command line, run under python3)
 # Then, here: python tools/collect_checkpoint.py TAG  (copies the summaries into profiles/).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,7 +24,7 @@ BENCH_ARGS=${BENCH_ARGS:---steps 20 --warmup 5}
 for s in $STAGES; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu \
+      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread ${TESTS:-tests} -m gpu \
         > gpurun_out/pytest_${TAG}.log 2>&1; rc=$?
       tail -2 gpurun_out/pytest_${TAG}.log
       [ $rc -eq 0 ] || { tail -40 gpurun_out/pytest_${TAG}.log; exit 1; } ;;
@@ -51,6 +54,10 @@ for s in $STAGES; do
       echo "pmcsum ok" ;;
     lds)
       bash tools/gpu_lds.sh ${TAG} || exit 1 ;;
+    probe)
+      timeout -k 10 ${PROBE_TIMEOUT:-300} python3 -u ${PROBE:?PROBE} > gpurun_out/probe_${TAG}.log 2>&1; rc=$?
+      grep -v amdgpu.ids gpurun_out/probe_${TAG}.log | tail -${PROBE_TAIL:-30}
+      [ $rc -eq 0 ] || exit 1 ;;
     *)
       echo "unknown stage $s"; exit 2 ;;
   esac
