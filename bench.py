@@ -426,6 +426,15 @@ def _roof_short(r):
     return out
 
 
+def _proxy_short(sp):
+    """of / ratio_min / speedup of the largest N, and the projected speedup at every N timed."""
+    out = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
+           "speedup": _sig(sp.get("projected_speedup"))}
+    if isinstance(sp.get("by_n"), dict):
+        out["speedup_by_n"] = {n: _sig(o.get("projected_speedup")) for n, o in sp["by_n"].items()}
+    return out
+
+
 def _leg_short(leg):
     if not isinstance(leg, dict):
         return None
@@ -433,15 +442,17 @@ def _leg_short(leg):
     wl = (leg.get("config") or {}).get("workload")
     if isinstance(wl, str):
         import re
-        out["workload"] = re.sub(r" \([^)]*\)", "", wl.split(";")[0])[:100]
+        w = re.sub(r" \([^)]*\)", "", wl.split(";")[0])
+        if len(w) > 140:  # cut at a clause boundary, never inside a token ("minSeedLen 19")
+            w = w[:140].rsplit(", ", 1)[0]
+        out["workload"] = w
     out["roofline"] = _roof_short(leg.get("roofline"))
     out["cpu_baseline"] = _cpu_short(leg.get("cpu_baseline"))
     if isinstance(leg.get("split_stats"), dict):
         out["fixups"] = leg["split_stats"].get("fixup_blocks")
     sp = leg.get("shard_proxy")
     if isinstance(sp, dict):
-        out["shard_proxy"] = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
-                              "speedup": _sig(sp.get("projected_speedup"))}
+        out["shard_proxy"] = _proxy_short(sp)
     return out
 
 
@@ -460,8 +471,7 @@ def headline(line: dict, detail_path=None) -> dict:
     h["cpu_baseline"] = _cpu_short(line.get("cpu_baseline"))
     sp = line.get("shard_proxy")
     if isinstance(sp, dict):
-        h["shard_proxy"] = {"of": sp.get("of"), "ratio_min": _sig(sp.get("ratio_min_vs_full")),
-                            "speedup": _sig(sp.get("projected_speedup"))}
+        h["shard_proxy"] = _proxy_short(sp)
     if isinstance(line.get("roofline_f64"), dict):
         h["roofline_f64_frac"] = _sig(line["roofline_f64"].get("frac"))
     if line.get("f32_only_gcups"):
@@ -639,29 +649,42 @@ def shard_note(args, what: str, lo: int, hi: int, total: int, world: int) -> str
 
 def proxy_on(args, world: int) -> bool:
     """The single-GPU proxy of the N-GPU strong-scaling run: on one GPU (world 1), time each shard
-    rank r of --shard-of N would get, with the same shard.py cut the N-rank run takes."""
-    return world == 1 and args.scaling == "strong" and args.shard_of > 1
+    rank r of an N-rank run would get (N in --shard-of), with the same shard.py cut that run takes."""
+    return world == 1 and args.scaling == "strong" and bool(args.shard_ns)
 
 
 def shard_proxy(args, full_ms: float, full_value: float, unit: str, time_rank):
-    """time_rank(r) -> (ms per step, per-GPU value) for rank r's shard of an --shard-of N job.
-    Returns each shard's per-GPU throughput, the lowest one against the full-set rate, and (all
-    ranks timed) the projected N-GPU strong-scaling speedup = full-set step / slowest shard step."""
-    ranks = range(args.shard_of) if args.shard_rank < 0 else [args.shard_rank]
-    per = []
-    for r in ranks:
-        ms, value = time_rank(r)
-        per.append({"rank": r, "ms_per_step": round(ms, 4), "value": round(value, 3)})
-    low = min(p["value"] for p in per)
-    out = {"of": args.shard_of, "unit": unit + " per GPU", "ranks": per, "per_gpu_min": low,
-           "ratio_min_vs_full": low / full_value if full_value else None,
+    """time_rank(r, n) -> (ms per step, per-GPU value) for rank r's shard of an n-rank job, for every
+    n in --shard-of (default 2, 4, 8: the metric's 1/2/4/8-GPU points). Per n: each shard's per-GPU
+    throughput, the lowest one against the full-set rate and (all ranks timed) the projected n-GPU
+    strong-scaling speedup = full-set step / slowest shard step. The top-level fields are the largest
+    n's; `by_n` carries every n."""
+    by_n = {}
+    for n in args.shard_ns:
+        ranks = range(n) if (args.shard_rank < 0 or n != args.shard_of) else [args.shard_rank]
+        per = []
+        for r in ranks:
+            ms, value = time_rank(r, n)
+            per.append({"rank": r, "ms_per_step": round(ms, 4), "value": round(value, 3)})
+        low = min(p["value"] for p in per)
+        one = {"of": n, "ranks": per, "per_gpu_min": low,
+               "ratio_min_vs_full": low / full_value if full_value else None}
+        if len(per) == n:
+            worst = max(p["ms_per_step"] for p in per)
+            one["projected_speedup"] = full_ms / worst
+            one["projected_efficiency"] = full_ms / worst / n
+        by_n[n] = one
+    top = by_n[args.shard_of]
+    out = {"of": args.shard_of, "unit": unit + " per GPU", "ranks": top["ranks"], "per_gpu_min": top["per_gpu_min"],
+           "ratio_min_vs_full": top["ratio_min_vs_full"],
            "note": f"1 GPU, world size 1: each rank's strong-scaling shard of the same set (shard.py) timed "
                    f"alone, {args.steps} steps after {args.warmup} warm-up; ratio = per-GPU rate on the "
-                   f"shard / full-set rate (>= 0.94 needed for 7.5x at 8)"}
-    if len(per) == args.shard_of:
-        worst = max(p["ms_per_step"] for p in per)
-        out["projected_speedup"] = full_ms / worst
-        out["projected_efficiency"] = full_ms / worst / args.shard_of
+                   f"shard / full-set rate (>= 0.94 needed for 7.5x at 8)",
+           "by_n": {str(n): {k: v for k, v in o.items() if k != "ranks"} | {"worst_ms": max(p["ms_per_step"] for p in o["ranks"])}
+                    for n, o in by_n.items()}}
+    for k in ("projected_speedup", "projected_efficiency"):
+        if k in top:
+            out[k] = top[k]
     return out
 
 
@@ -856,10 +879,10 @@ def bench_chain(args, D, rank, world, kind="large"):
         out["rank_check"] = rank_check(args, D, rank, world, f"chain {kind}", shard.digest(keys, *r4), len(keys),
                                        full_pass)
     if proxy_on(args, world):
-        log(f"chain {kind}: shard proxy of {args.shard_of}")
+        log(f"chain {kind}: shard proxies of {args.shard_ns}")
 
-        def t_rank(r):
-            sub, _ = shard.shard_calls(full, r, args.shard_of)
+        def t_rank(r, n):
+            sub, _ = shard.shard_calls(full, r, n)
             sb = chain.ChainBatch(sub)
             for _ in range(1 + args.warmup):
                 sb.run()
@@ -1050,10 +1073,10 @@ def bench_bsw(args, D, rank, world, kind="large"):
         out["rank_check"] = rank_check(args, D, rank, world, f"bsw {kind}", shard.digest(keys, *o6.T), pairs.n,
                                        full_pass)
     if proxy_on(args, world):
-        log(f"bsw {kind}: shard proxy of {args.shard_of}")
+        log(f"bsw {kind}: shard proxies of {args.shard_ns}")
 
-        def t_rank(r):
-            sub, _ = shard.shard_pairs(full, r, args.shard_of)
+        def t_rank(r, n):
+            sub, _ = shard.shard_pairs(full, r, n)
             sb = bsw.BswBatch(sub, params)
             for _ in range(1 + args.warmup):
                 sb.run()
@@ -1194,10 +1217,10 @@ def bench_phmm(args, D, rank, world, kind="large"):
         out["rank_check"] = rank_check(args, D, rank, world, f"phmm {kind}",
                                        shard.digest(tidx, res[:ta.n], used[:ta.n]), ta.n, full_pass)
     if proxy_on(args, world):
-        log(f"phmm {kind}: shard proxy of {args.shard_of}")
+        log(f"phmm {kind}: shard proxies of {args.shard_ns}")
 
-        def t_rank(r):
-            sub, _ = shard.shard_testcases(full, r, args.shard_of)
+        def t_rank(r, n):
+            sub, _ = shard.shard_testcases(full, r, n)
             sj = phmm.DeviceBatch(sub)
             for _ in range(1 + args.warmup):
                 sj.run()
@@ -1464,10 +1487,10 @@ def fmi_rank_check(args, D, rank, world, what, fmi, shard, idx, rs, codes_all, l
 
 
 def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full_value):
-    log(f"fmi: shard proxy of {args.shard_of}")
+    log(f"fmi: shard proxies of {args.shard_ns}")
 
-    def t_rank(r):
-        lo, hi = shard.read_range(len(lens_all), r, args.shard_of)
+    def t_rank(r, n):
+        lo, hi = shard.read_range(len(lens_all), r, n)
         rs = fmi.Reads(idx, codes_all[lo:hi], lens_all[lo:hi])
         for _ in range(1 + args.warmup):
             rs.search(19)
@@ -1737,14 +1760,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end (host arrays) timings")
-    ap.add_argument("--shard-of", type=int, default=8,
+    ap.add_argument("--shard-of", default="2,4,8",
                     help="single-GPU proxy (world size 1, strong scaling): also time the shards an N-GPU run "
-                         "would give its ranks (0 or 1 = off)")
+                         "would give its ranks, for each N of the comma list ('' or 0 = off)")
     ap.add_argument("--shard-rank", type=int, default=-1, help="proxy only this rank's shard (-1 = every rank)")
     ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
                     help="where the full record goes (shard proxies, drop-ins, traffic detail, parity checks); "
                          "stdout carries only the compact headline line ('' = no file)")
     args = ap.parse_args()
+    args.shard_ns = sorted({int(x) for x in str(args.shard_of).split(",") if x.strip() and int(x) > 1})
+    args.shard_of = max(args.shard_ns) if args.shard_ns else 0
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" in os.environ:
