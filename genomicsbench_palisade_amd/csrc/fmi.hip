@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
       }
     }
     if (nout < cap) {
-      gb_smem e;
+      gb_smem e{};  // zeroed: the 4 padding bytes after n are part of the output records
       e.rid = (uint32_t)rd;
       e.m = m;
       e.n = n;
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(64) void smem_heavy(HeavyArgs A) {
       }
       if (nout < cap) {
         if (lane == 0) {
-          gb_smem e;
+          gb_smem e{};  // zeroed: the 4 padding bytes after n are part of the output records
           e.rid = (uint32_t)rd;
           e.m = m;
           e.n = n;

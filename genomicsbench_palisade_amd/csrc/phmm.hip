@@ -1106,10 +1106,25 @@ struct StageLayout {
   }
 };
 
+// The limits of include/gb_phmm.h, checked before any device work; the error names the first bad
+// testcase by its index in the caller's array.
+int validate_testcases(const gb_testcase *tcs, int n) {
+  for (int k = 0; k < n; k++) {
+    const gb_testcase &t = tcs[k];
+    GB_ARG(t.rslen >= 1 && t.rslen <= 65535, "testcase %d: rslen %d outside [1,65535]", k, t.rslen);
+    GB_ARG(t.haplen >= 1 && t.haplen <= kMaxHaplen, "testcase %d: haplen %d outside [1,%d]", k,
+           t.haplen, kMaxHaplen);
+    GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
+  }
+  return GB_OK;
+}
+
 // Pack the testcases (deduplicated reads/haplotypes, stacks in LPT order) into b's pinned staging
 // buffer and upload them, growing its buffers when they are too small; b's stream/events exist
 // already. threads: host threads of the pack and merge phases (0: up to 8 from pack_min testcases).
-int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0) {
+// validated: the caller has run validate_testcases over the whole call (compute_pipelined, whose
+// chunks would otherwise name a testcase by its index in the chunk).
+int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0, bool validated = false) {
   HostClock clk;
   // Pack: deduplicate reads and haplotypes by pointer (the driver shares them across the R x H
   // cross product, PairHMMUnitTest.cpp:564-579), convert bases to codes once. Inputs are validated
@@ -1118,13 +1133,8 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0)
   // concatenated and haplotype ids are made global in first-appearance order, which is the id order
   // a single pass gives (a read shared across a chunk edge is stored once per chunk). Descriptors,
   // stack lists, stacks and pool are written straight into the pinned staging buffer.
-  for (int k = 0; k < n; k++) {
-    const gb_testcase &t = tcs[k];
-    GB_ARG(t.rslen >= 1 && t.rslen <= 65535, "testcase %d: rslen %d outside [1,65535]", k, t.rslen);
-    GB_ARG(t.haplen >= 1 && t.haplen <= kMaxHaplen, "testcase %d: haplen %d outside [1,%d]", k,
-           t.haplen, kMaxHaplen);
-    GB_ARG(t.rs && t.q && t.i && t.d && t.c && t.hap, "testcase %d: null sequence pointer", k);
-  }
+  if (!validated)
+    if (int st = validate_testcases(tcs, n)) return st;
   clk.mark("validate");
   // calls from 8 K testcases pack on several threads (2 K testcases each at least): the reference's
   // per-batch calls (PairHMMUnitTest.cpp:549-593) are mostly 5-45 K testcases
@@ -1508,13 +1518,16 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     B[c]->force_f64 = false;
   }
   HostClock clk;
+  // the whole call is validated here, before any chunk is packed or launched: a bad testcase fails the
+  // call with its index in the caller's array and nothing on the device
+  if ((st = validate_testcases(tcs, n))) return st;
   // host threads: about 12 over the concurrent fills (GB_PHMM_FILL_THREADS: per fill)
   int fill_threads = std::max(1, 12 / k);
   if (const char *f = getenv("GB_PHMM_FILL_THREADS")) fill_threads = std::max(1, atoi(f));
   const int device = tabs->device;
   auto fill = [&, device](int c) -> std::pair<int, std::string> {
     if (hipSetDevice(device) != hipSuccess) return {GB_ERR_HIP, "gb_phmm_compute: hipSetDevice failed"};
-    const int s = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c], fill_threads);
+    const int s = batch_fill(B[c], tcs + lo[c], lo[c + 1] - lo[c], fill_threads, true);
     return {s, s ? std::string(gb::last_error()) : std::string()};
   };
   // the workers' futures join on destruction, also on an early return
@@ -1525,9 +1538,22 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     return gb_phmm_batch_results(B[c], results ? results + o : nullptr, raw_f ? raw_f + o : nullptr,
                                  raw_d ? raw_d + o : nullptr, used_double ? used_double + o : nullptr, nullptr);
   };
-  if ((st = batch_fill(B[0], tcs, lo[1], fill_threads))) return st;
+  // on an error, the chunks already launched are waited for before the call returns, so no kernel
+  // of this call is left in flight (results are undefined on a nonzero status) and the next call
+  // refills those workspaces behind nothing
+  int launched = 0;
+  auto fail = [&](int s) {
+    const std::string msg = gb::last_error();
+    for (int c = 0; c < launched; c++) (void)hipStreamSynchronize(B[c]->stream);
+    for (size_t c = 0; c < ready.size(); c++)
+      if (ready[c].valid()) ready[c].wait();
+    gb::set_error("%s", msg.c_str());
+    return s;
+  };
+  if ((st = batch_fill(B[0], tcs, lo[1], fill_threads, true))) return fail(st);
   clk.mark("chunk 0 filled");
-  if ((st = gb_phmm_batch_run(B[0]))) return st;
+  if ((st = gb_phmm_batch_run(B[0]))) return fail(st);
+  launched = 1;
   // chunk c - 2's results are fetched after chunk c is launched: the host never waits on the chunk
   // the GPU has just started, only on one queued behind it
   int fetched = 0;
@@ -1535,17 +1561,18 @@ int compute_pipelined(DeviceTables *tabs, const gb_testcase *tcs, int n, double 
     const auto r = ready[c - 1].get();
     if (r.first) {
       gb::set_error("%s", r.second.c_str());
-      return r.first;
+      return fail(r.first);
     }
     clk.mark("chunk ready");
-    if ((st = gb_phmm_batch_run(B[c]))) return st;
+    if ((st = gb_phmm_batch_run(B[c]))) return fail(st);
+    launched = c + 1;
     if (c >= 2) {
-      if ((st = fetch(fetched++))) return st;
+      if ((st = fetch(fetched++))) return fail(st);
       clk.mark("chunk fetched");
     }
   }
   while (fetched < k)
-    if ((st = fetch(fetched++))) return st;
+    if ((st = fetch(fetched++))) return fail(st);
   clk.mark("last chunks fetched");
   return st;
 }

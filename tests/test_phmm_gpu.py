@@ -270,3 +270,21 @@ def test_rows_per_lane_ab_identical(phmm, monkeypatch):
         outs.append(phmm.compute_likelihoods_both(ta))
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert (bits(a) == bits(b)).all()
+
+
+@pytest.mark.parametrize("where", ["chunk2", "last"])
+def test_pipelined_bad_testcase_reports_its_index(phmm, monkeypatch, where):
+    """A bad testcase in a later chunk of a pipelined call fails the whole call before any device
+    work, and the error names its index in the caller's array (the call is validated on the calling
+    thread before it is cut into chunks); the next call on the same workspaces is exact."""
+    from genomicsbench_palisade_amd import GbError
+    monkeypatch.setenv("GB_PHMM_PIPE", "4")
+    rng = np.random.default_rng(47)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(4)])
+    n = ta.n
+    bad = (n * 3 // 10 + 7) if where == "chunk2" else n - 2  # chunk weights 1:2:3:4 of n
+    ta.arr[bad].haplen = 70000
+    with pytest.raises(GbError, match=f"testcase {bad}: haplen 70000"):
+        phmm.compute_likelihoods_both(ta)
+    ok = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(4)])
+    assert_exact(phmm.compute_likelihoods_both(ok), oracle_run(ok))

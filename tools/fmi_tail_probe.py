@@ -24,6 +24,7 @@ idx = fmi.Index.build(ref)
 codes, lens = gen.fmi_reads(ref, nreads, read_len=151, seed=8)
 L = lib()
 L.gb_fmi_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+L.gb_fmi_debug_trace_rows.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 out = {}
 for name, (lo, hi) in [("shard0", shard.read_range(nreads, 0, of)), ("full", (0, nreads))]:
     rs = fmi.Reads(idx, codes[lo:hi], lens[lo:hi])
@@ -40,9 +41,11 @@ for name, (lo, hi) in [("shard0", shard.read_range(nreads, 0, of)), ("full", (0,
     rs.search(19)
     rs.sync()
     at, _, _ = rs.timing()
-    tr = np.zeros(3 * (hi - lo), np.int64)
+    rows = ctypes.c_int64()
+    L.gb_fmi_debug_trace_rows(rs.h, ctypes.byref(rows))
+    tr = np.zeros(3 * rows.value, np.int64)
     L.gb_fmi_debug_trace(rs.h, tr.ctypes.data)
-    tr = tr.reshape(-1, 3)
+    tr = tr.reshape(-1, 3)  # one row per task: reads, then (split search) their LAST tasks
     rs.close()
     hv = tr[:, 2] < 0  # reads redone by smem_heavy (calls negated)
     tr[:, 2] = np.abs(tr[:, 2])
@@ -71,6 +74,11 @@ for name, (lo, hi) in [("shard0", shard.read_range(nreads, 0, of)), ("full", (0,
           f"last take {last_start:.2f} ms; read ms p50 {np.percentile(dur, 50):.2f} p99 {np.percentile(dur, 99):.2f} "
           f"max {dur.max():.2f}; ext p50 {np.percentile(c, 50):.0f} p99 {np.percentile(c, 99):.0f} max {c.max()}; "
           f"slowest-ending read: start {st[k] * 1e-5:.2f} ms, {dur[k]:.2f} ms, {c[k]} ext", flush=True)
+    if len(tr) > hi - lo:  # split search: the LAST tasks
+        lt = slice(hi - lo, None)
+        print(f"  split: LAST tasks take {st[lt].min() * 1e-5:.2f}..{st[lt].max() * 1e-5:.2f} ms, end by "
+              f"{en[lt].max() * 1e-5:.2f} ms, ms p50 {np.percentile(dur[lt], 50):.2f} max {dur[lt].max():.2f}; "
+              f"search tasks end by {en[:hi - lo].max() * 1e-5:.2f} ms", flush=True)
     if name == "shard0":
         out = dict(st=st.astype(np.int32), en=en.astype(np.int32), calls=c.astype(np.int32), heavy=hv)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
