@@ -1378,6 +1378,52 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0,
   }
   Stack *h_stacks = (Stack *)(b->h_stage + L.o_stk);
   for (int k = 0; k < ns_all; k++) h_stacks[k] = stacks[(uint32_t)key[k]];
+  // Tail split: the stacks holding the last 10 % of the LPT order's cost are cut into stacks of at
+  // most 512 rows (taller stacks waste less on the anti-diagonal fill; shorter ones let the grid's
+  // last waves end together). Measured (tools/phmm_shard_probe.py, profiles/r06h/r06i): the 'large'
+  // job 31.93-32.00 -> 31.65 ms, its 1/8 shard 4.47-4.49 -> 4.41-4.46 ms; 5 / 15 / 20 / 30 % and
+  // 128 / 256 / 384-row pieces no better on the job. GB_PHMM_TAIL=frac:rows (0 = off) for probes.
+  double frac = stack_rows > 512 ? 0.10 : 0.0;
+  int trows = 512;
+  if (const char *te = getenv("GB_PHMM_TAIL")) {
+    frac = atof(te);
+    const char *cm = strchr(te, ':');
+    if (cm) trows = std::max(1, atoi(cm + 1));
+  }
+  if (frac > 0) {
+    const int ns_short = ns_all - n_long;
+    auto cost_of = [&](const Stack &S) -> uint64_t {
+      int rows = 0;
+      for (uint32_t t = 0; t < S.count; t++) rows += (int)(desc[order[S.first + t]].dims & 0xffff) + 2;
+      return (uint64_t)((rows + sh - 1) / sh) * (uint64_t)(S.C + sh);
+    };
+    uint64_t total = 0;
+    for (int k = 0; k < ns_short; k++) total += cost_of(h_stacks[k]);
+    uint64_t acc = 0;
+    int t0 = ns_short;
+    while (t0 > 0 && (double)acc < frac * (double)total) acc += cost_of(h_stacks[--t0]);
+    std::vector<std::pair<uint64_t, Stack>> pieces;
+    for (int k = t0; k < ns_short; k++) {
+      const Stack S = h_stacks[k];
+      uint32_t t = 0;
+      while (t < S.count) {
+        Stack P{S.first + t, 0, S.hap_off, S.C};
+        int rows = 0;
+        while (t < S.count && (P.count == 0 || rows + (int)(desc[order[S.first + t]].dims & 0xffff) + 2 <= trows)) {
+          rows += (int)(desc[order[S.first + t]].dims & 0xffff) + 2;
+          P.count++;
+          t++;
+        }
+        pieces.push_back({(uint64_t)((rows + sh - 1) / sh) * (uint64_t)(S.C + sh), P});
+      }
+    }
+    std::stable_sort(pieces.begin(), pieces.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+    std::vector<Stack> longs(h_stacks + ns_short, h_stacks + ns_all);
+    int k = t0;
+    for (const auto &pc : pieces) h_stacks[k++] = pc.second;
+    for (const auto &ls : longs) h_stacks[k++] = ls;
+    ns_all = k;
+  }
   clk.mark("stacks");
   if (int st = batch_reserve(b, n, pool_bytes)) return st;
   if (n_long) {

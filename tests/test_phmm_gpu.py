@@ -288,3 +288,21 @@ def test_pipelined_bad_testcase_reports_its_index(phmm, monkeypatch, where):
         phmm.compute_likelihoods_both(ta)
     ok = TestcaseArray.from_batches([gen.phmm_batch(rng, 30, 12) for _ in range(4)])
     assert_exact(phmm.compute_likelihoods_both(ok), oracle_run(ok))
+
+
+@pytest.mark.parametrize("tail", ["0", "0.9:64", "1.0:1", "0.5:300"])
+def test_tail_split_stacks_exact(phmm, monkeypatch, tail):
+    """The LPT tail split (csrc/phmm.hip batch_fill: the stacks holding the last part of the cost cut
+    into shorter stacks; default 10 % into <= 512 rows on jobs of taller stacks) forced over most of a
+    job, down to one testcase per stack, with 1024-row stacks before it: bit-exact, both passes."""
+    monkeypatch.setenv("GB_PHMM_TAIL", tail)
+    monkeypatch.setenv("GB_PHMM_STACK_ROWS", "1024")
+    rng = np.random.default_rng(53)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 60, 24) for _ in range(3)])
+    exp = oracle_run(ta)
+    assert (exp[1] < 1e-28).any()
+    assert_exact(phmm.compute_likelihoods_both(ta), exp)
+    db = phmm.DeviceBatch(ta)
+    db.run()
+    assert_exact(db.results()[:4], exp)
+    db.close()

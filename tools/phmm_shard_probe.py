@@ -22,7 +22,7 @@ of, r = int(os.environ.get("PHMM_OF", "8")), int(os.environ.get("PHMM_RANK", "0"
 for name, ta in [("full", full), (f"shard {r}/{of}", shard.shard_testcases(full, r, of)[0])]:
     for rows in os.environ.get("PHMM_ROWS", "default").split(";"):
         # a setting: "default", a GB_PHMM_STACK_ROWS value, or env assignments "K=V,K=V"
-        for k in ("GB_PHMM_STACK_ROWS", "GB_PHMM_F64_ROWS", "GB_PHMM_RPL", "GB_PHMM_W2", "GB_PHMM_PIPE",
+        for k in ("GB_PHMM_STACK_ROWS", "GB_PHMM_F64_ROWS", "GB_PHMM_RPL", "GB_PHMM_W2", "GB_PHMM_PIPE", "GB_PHMM_TAIL",
                   "GB_PHMM_F64_REGROUP", "GB_PHMM_F64_PARTS"):
             os.environ.pop(k, None)
         if "=" in rows:
