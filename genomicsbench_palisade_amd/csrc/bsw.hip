@@ -772,8 +772,11 @@ int bsw_batch_fill(gb_bsw_batch *B, const gb_bsw_params *params, const gb_seqpai
     // r03ab, 100 k pairs: 0 228, 0.05 234, 0.1 258, 0.2 243 GCUPS. A batch of fewer lane waves than
     // SIMDs (the 1/8 shard of the 'small' set: 12.5 k pairs, 195 waves on 1 024 SIMDs) is one wave's
     // critical path long: every lane pair goes to the wave-per-pair kernel (1.30 -> 0.56 ms,
-    // profiles/r05b_bsw_small.log)
-    const double frac = te ? atof(te) : (n < (int64_t)64 * 4 * std::max(B->num_cus, 1) ? 1.0 : 0.1);
+    // profiles/r05b_bsw_small.log). The crossover against the 0.1 split, swept on the 'large' pair
+    // distribution (profiles/r06j/r06k_bsw_tail_*.txt, 256 CUs): all-to-wave wins from 8 K to 65 536
+    // pairs (49 152: 1.19 vs 1.79 ms; 65 536: 1.52 vs 1.65) and loses from 80 000 (1.79 vs 1.64 ms),
+    // so the rule is n < 64 x 4.5 x CUs (73 728 pairs)
+    const double frac = te ? atof(te) : (2 * n < (int64_t)64 * 9 * std::max(B->num_cus, 1) ? 1.0 : 0.1);
     const int64_t fill = (int64_t)64 * 8 * std::max(B->num_cus, 1);  // lane waves of 64 pairs, 2 per SIMD
     if (frac > 0 && (n >= 1024 || frac >= 1.0) && n <= 2 * fill) {
       std::vector<uint32_t> cost;
