@@ -1201,7 +1201,17 @@ int small_group(SmallWs *W, const std::vector<SmallReq *> &g) {
 // fewer than kLeaders groups in flight takes every queued request with the same parameters and runs
 // them as one launch, the others wait for their request to be marked done. While one group runs, the
 // next one accumulates, so groups grow to about one call per waiting thread.
-constexpr int kLeaders = 2;  // groups in flight per device (one packing/copying while one computes)
+// groups in flight per device (packing / copying while others compute): getScores16 per 512 pairs
+// from 16 threads, 2 M pairs: 1 / 2 / 3 / 4 / 6 groups 40.3 / 48.6 / 52.4 / 52.9 / 49.1 GCUPS
+// (profiles/r06u_bsw_leaders.txt)
+constexpr int kLeaders = 4;
+int leaders_limit() {  // GB_BSW_LEADERS (probes)
+  static const int v = [] {
+    const char *e = getenv("GB_BSW_LEADERS");
+    return e ? std::max(1, atoi(e)) : kLeaders;
+  }();
+  return v;
+}
 
 struct Combiner {
   std::mutex m;
@@ -1240,7 +1250,7 @@ int small_call(const gb_bsw_params *params, gb_seqpair *pairs, int64_t n, const 
   std::unique_lock<std::mutex> lk(C.m);
   C.pending.push_back(&me);
   while (!me.done) {
-    if (C.leaders < kLeaders && !C.pending.empty()) {
+    if (C.leaders < leaders_limit() && !C.pending.empty()) {
       // lead: take the queued requests with the first one's parameters (up to kSmallCall pairs)
       std::vector<SmallReq *> g, rest;
       int64_t np = 0;
