@@ -653,6 +653,19 @@ def proxy_on(args, world: int) -> bool:
     return world == 1 and args.scaling == "strong" and bool(args.shard_ns)
 
 
+def proxy_warm(args, one) -> int:
+    """Warm-up of one shard of the proxy: one() runs a step to completion, at least 1 + --warmup times
+    and for at least --proxy-warm-ms. A 1/8 shard's step is a few ms, so --warmup steps alone end
+    while the GPU is still raising its clocks (phmm 1/8 shard: 4.95 -> 4.2 ms per step over its first
+    ~50 ms, profiles/r06y_phmm_shard_ramp.txt) and the proxy timed that ramp, not the shard; an N-GPU
+    run's ranks run their shards back to back. Returns the warm-up steps run."""
+    t0, k = time.perf_counter(), 0
+    while k < 1 + args.warmup or (time.perf_counter() - t0) * 1e3 < args.proxy_warm_ms:
+        one()
+        k += 1
+    return k
+
+
 def shard_proxy(args, full_ms: float, full_value: float, unit: str, time_rank):
     """time_rank(r, n) -> (ms per step, per-GPU value) for rank r's shard of an n-rank job, for every
     n in --shard-of (default 2, 4, 8: the metric's 1/2/4/8-GPU points). Per n: each shard's per-GPU
@@ -678,7 +691,8 @@ def shard_proxy(args, full_ms: float, full_value: float, unit: str, time_rank):
     out = {"of": args.shard_of, "unit": unit + " per GPU", "ranks": top["ranks"], "per_gpu_min": top["per_gpu_min"],
            "ratio_min_vs_full": top["ratio_min_vs_full"],
            "note": f"1 GPU, world size 1: each rank's strong-scaling shard of the same set (shard.py) timed "
-                   f"alone, {args.steps} steps after {args.warmup} warm-up; ratio = per-GPU rate on the "
+                   f"alone, {args.steps} steps after >= {1 + args.warmup} warm-up steps and >= "
+                   f"{args.proxy_warm_ms:g} ms of them; ratio = per-GPU rate on the "
                    f"shard / full-set rate (>= 0.94 needed for 7.5x at 8)",
            "by_n": {str(n): {k: v for k, v in o.items() if k != "ranks"} | {"worst_ms": max(p["ms_per_step"] for p in o["ranks"])}
                     for n, o in by_n.items()}}
@@ -884,9 +898,7 @@ def bench_chain(args, D, rank, world, kind="large"):
         def t_rank(r, n):
             sub, _ = shard.shard_calls(full, r, n)
             sb = chain.ChainBatch(sub)
-            for _ in range(1 + args.warmup):
-                sb.run()
-                sb.sync()
+            proxy_warm(args, lambda: (sb.run(), sb.sync()))
 
             def st():
                 sb.run()
@@ -1078,9 +1090,7 @@ def bench_bsw(args, D, rank, world, kind="large"):
         def t_rank(r, n):
             sub, _ = shard.shard_pairs(full, r, n)
             sb = bsw.BswBatch(sub, params)
-            for _ in range(1 + args.warmup):
-                sb.run()
-                sb.sync()
+            proxy_warm(args, lambda: (sb.run(), sb.sync()))
             c = sb.results(want_cells=False)[2]
 
             def st():
@@ -1222,8 +1232,7 @@ def bench_phmm(args, D, rank, world, kind="large"):
         def t_rank(r, n):
             sub, _ = shard.shard_testcases(full, r, n)
             sj = phmm.DeviceBatch(sub)
-            for _ in range(1 + args.warmup):
-                sj.run()
+            proxy_warm(args, lambda: (sj.run(), sj.sync()))
             el, _ = timed_steps(D, args.steps, sj.run, lambda: (sj.sync(), 0.0)[1])
             c = sj.stats()[1]
             sj.close()
@@ -1492,9 +1501,7 @@ def fmi_shard_proxy(args, D, fmi, shard, idx, codes_all, lens_all, full_ms, full
     def t_rank(r, n):
         lo, hi = shard.read_range(len(lens_all), r, n)
         rs = fmi.Reads(idx, codes_all[lo:hi], lens_all[lo:hi])
-        for _ in range(1 + args.warmup):
-            rs.search(19)
-            rs.sync()
+        proxy_warm(args, lambda: (rs.search(19), rs.sync()))
 
         def st():
             rs.search(19)
@@ -1764,6 +1771,8 @@ def main():
                     help="single-GPU proxy (world size 1, strong scaling): also time the shards an N-GPU run "
                          "would give its ranks, for each N of the comma list ('' or 0 = off)")
     ap.add_argument("--shard-rank", type=int, default=-1, help="proxy only this rank's shard (-1 = every rank)")
+    ap.add_argument("--proxy-warm-ms", type=float, default=150.0,
+                    help="proxy: each shard's warm-up runs at least this long (and at least 1 + --warmup steps)")
     ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
                     help="where the full record goes (shard proxies, drop-ins, traffic detail, parity checks); "
                          "stdout carries only the compact headline line ('' = no file)")

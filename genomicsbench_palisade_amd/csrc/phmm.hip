@@ -53,6 +53,12 @@ constexpr int kBndPad = 72;  // boundary records beyond column C (see phmm_strip
 constexpr int kRecPad = 4;   // boundary records below column 0 (lane 63's writes start at column -2)
 constexpr int kQualTab = 128;
 constexpr int kStackRows = 2048;  // rows per stack (a testcase taller than this gets its own)
+// the batch's device counter words (d_count): [0..7] the passes' counters, then the f64 plan's
+// bucket counts, bucket cursors and its number of units with work (f64_plan)
+constexpr int kPlanBuckets = 128;
+constexpr int kPlanCount = 8, kPlanCursor = kPlanCount + kPlanBuckets, kPlanTotal = kPlanCursor + kPlanBuckets;
+constexpr int kCountWords = kPlanTotal + 8;
+constexpr int kMaxF64Parts = 8;
 constexpr int kM2M = ((127 * 128) >> 1) + 128;  // set_mm_prob indices for quals < 128
 
 // ---------------------------------------------------------------------------------------------
@@ -799,7 +805,7 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
                                                     const uint8_t *__restrict__ pool, DevTab<T> tab,
                                                     T *__restrict__ raw_out, const float *__restrict__ raw_f,
                                                     int *__restrict__ counter, int force, uint8_t *scratch,
-                                                    size_t scratch_stride) {
+                                                    size_t scratch_stride, const uint32_t *__restrict__ units) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   uint8_t *rec = kLong ? scratch + (size_t)blockIdx.x * scratch_stride : smem_raw;
   if constexpr (kF64Pass || kLong) {
@@ -808,11 +814,14 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
     // f64 pass over the LDS stacks: `parts` work units per stack (the top byte of `force`), so a job
     // of few stacks per worker balances its fallback work finer
     const int parts = (kF64Pass && !kLong) ? max(1, (force >> 8) & 0xFF) : 1;
+    // with a plan (f64_plan / f64_plan_order): only the units that have work, costliest first
+    const int nwork = units ? __builtin_amdgcn_readfirstlane(counter[kPlanTotal]) : nstacks * parts;
     while (true) {
       int k = 0;
       if (threadIdx.x == 0) k = atomicAdd(next, 1);
       k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-      if (k >= nstacks * parts) break;
+      if (k >= nwork) break;
+      if (units) k = __builtin_amdgcn_readfirstlane((int)units[k]);
       done += phmm_stack<T, kF64Pass>(stacks[k / parts], stk_tc, descs, pool, tab, raw_out, raw_f, (force & 0xFF) != 0,
                                       rec, k % parts, parts);
       __syncthreads();  // the next stack re-initialises the records
@@ -822,6 +831,69 @@ __global__ __launch_bounds__(64) void phmm_forward(const Stack *__restrict__ sta
     phmm_stack<T, false, kExit>(stacks[blockIdx.x], stk_tc, descs, pool, tab, raw_out, nullptr, false, rec, 0, 1,
                                 reinterpret_cast<unsigned long long *>(counter + 4));
   }
+}
+
+// f64 pass plan: the persistent grid's units (stack parts) ordered by their cost, costliest first, so
+// the grid's tail is its cheapest units -- a 1/8 shard's f64 pass has only ~8 units per resident
+// wave, and ordered by the f32 pass's stack order (its rows, not the fallback's) its last units were
+// as long as any. f64_plan: per unit the stripes of its fallback rows times the columns a stripe
+// sweeps, as a bucket key (0: no fallback row), and the buckets' counts; f64_plan_order: the units
+// with work into `units`, by descending key (any order inside a bucket: a unit's outputs do not
+// depend on when it runs).
+__global__ __launch_bounds__(256) void f64_plan(const Stack *__restrict__ stacks, int nunits, int parts,
+                                                const uint32_t *__restrict__ stk_tc, const TcDesc *__restrict__ descs,
+                                                const float *__restrict__ raw_f, int force, uint8_t *__restrict__ ukey,
+                                                int *__restrict__ counter) {
+  __shared__ int hist[kPlanBuckets];
+  for (int i = threadIdx.x; i < kPlanBuckets; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < nunits) {
+    const Stack S = stacks[u / parts];
+    const int part = u % parts, lo = part * (int)S.count / parts, hi = (part + 1) * (int)S.count / parts;
+    int rows = 0;
+    for (int a = lo; a < hi; a++) {
+      const TcDesc d = descs[stk_tc[S.first + a]];
+      if (force || raw_f[d.out_idx] < 1e-28f) rows += (int)(d.dims & 0xffff) + 2;  // as phmm_stack's `act`
+    }
+    int key = 0;
+    if (rows) {
+      key = (((rows + kWave - 1) / kWave) * ((int)S.C + kWave) + 63) / 64;
+      key = key < 1 ? 1 : (key > kPlanBuckets - 1 ? kPlanBuckets - 1 : key);
+      atomicAdd(&hist[key], 1);
+    }
+    ukey[u] = (uint8_t)key;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPlanBuckets; i += blockDim.x)
+    if (hist[i]) atomicAdd(&counter[kPlanCount + i], hist[i]);
+}
+
+__global__ __launch_bounds__(256) void f64_plan_order(int nunits, const uint8_t *__restrict__ ukey,
+                                                      int *__restrict__ counter, uint32_t *__restrict__ units) {
+  __shared__ int cnt[kPlanBuckets], off[kPlanBuckets], hist[kPlanBuckets], base[kPlanBuckets];
+  for (int i = threadIdx.x; i < kPlanBuckets; i += blockDim.x) {
+    cnt[i] = counter[kPlanCount + i];
+    hist[i] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // bucket offsets, descending key
+    int sum = 0;
+    for (int k = kPlanBuckets - 1; k >= 1; k--) {
+      off[k] = sum;
+      sum += cnt[k];
+    }
+    if (blockIdx.x == 0) counter[kPlanTotal] = sum;
+  }
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  const int key = u < nunits ? ukey[u] : 0;
+  int rank = 0;
+  if (key) rank = atomicAdd(&hist[key], 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPlanBuckets; i += blockDim.x)
+    if (hist[i]) base[i] = atomicAdd(&counter[kPlanCursor + i], hist[i]);
+  __syncthreads();
+  if (key) units[off[key] + base[key] + rank] = (uint32_t)u;
 }
 
 // gb_phmm_init's warm-up launch (no work)
@@ -967,7 +1039,10 @@ struct gb_phmm_batch {
   size_t scratch_stride = 0, cap_scratch = 0;
   int *d_count = nullptr;  // [0] testcases recomputed by the f64 pass, [1] its stack counter,
                            // [4..7] the f32 early exit's two u64 counts (testcases, cells skipped),
-                           // [2] / [3] the kLong f32 / f64 stack counters
+                           // [2] / [3] the kLong f32 / f64 stack counters, then the f64 plan's words
+                           // (kCountWords in all)
+  uint32_t *d_units = nullptr;  // f64 plan: units with work, costliest first (kMaxF64Parts per testcase)
+  uint8_t *d_ukey = nullptr;    // f64 plan: per unit its cost bucket
   size_t cap_n = 0, cap_pool = 0;  // allocated capacities (a cached workspace batch is refilled)
   int f64_grid = 0;                // persistent f64 grid: resident workgroups of the device
   int cus = 256;                   // compute units of the device (stack height rule)
@@ -976,6 +1051,7 @@ struct gb_phmm_batch {
   int rpl = 1;  // rows per lane of the f32 pass over LDS stacks (GB_PHMM_RPL=2: two, for A/B probes)
   int w2 = 0;   // its register budget: waves per SIMD 0 (compiler), 6 or 8 (GB_PHMM_W2, probes)
   int f64_parts = 2;  // work units per stack in the f64 pass (GB_PHMM_F64_PARTS)
+  bool f64_plan = true;  // the f64 pass's units by cost (f64_plan; GB_PHMM_F64_PLAN=0: stack order)
   bool f32_exit = true;  // the f32 pass's early exit (phmm_stack kExit; GB_PHMM_EXIT=0 turns it off)
   // host scratch of the fills (grow-only, host_reserve)
   std::vector<uint32_t> hid;
@@ -1028,12 +1104,15 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
     b->d_rd = b->d_out = nullptr;
     b->d_stk_tc = nullptr;
     b->d_stacks = nullptr;
+    b->d_units = nullptr;
+    b->d_ukey = nullptr;
     b->cap_n = 0;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t sz[6] = {up(sizeof(TcDesc) * nn), up(sizeof(float) * nn), up(sizeof(double) * nn),
+    const size_t sz[8] = {up(sizeof(TcDesc) * nn), up(sizeof(float) * nn), up(sizeof(double) * nn),
                           up(sizeof(double) * nn), up(sizeof(uint32_t) * nn),
-                          up(sizeof(Stack) * nn)};  // at most one stack per testcase
-    GB_HIP(hipMalloc(&b->d_arena, sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5]));
+                          up(sizeof(Stack) * nn),  // at most one stack per testcase
+                          up(sizeof(uint32_t) * nn * kMaxF64Parts), up(nn * kMaxF64Parts)};
+    GB_HIP(hipMalloc(&b->d_arena, sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5] + sz[6] + sz[7]));
     uint8_t *a = (uint8_t *)b->d_arena;
     b->d_desc = (TcDesc *)a;
     a += sz[0];
@@ -1046,6 +1125,10 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
     b->d_stk_tc = (uint32_t *)a;
     a += sz[4];
     b->d_stacks = (Stack *)a;
+    a += sz[5];
+    b->d_units = (uint32_t *)a;
+    a += sz[6];
+    b->d_ukey = a;
     b->cap_n = nn;
   }
   if (pool_bytes > b->cap_pool) {
@@ -1055,7 +1138,7 @@ int batch_reserve(gb_phmm_batch *b, int n, size_t pool_bytes) {
     GB_HIP(hipMalloc(&b->d_pool, pool_bytes));
     b->cap_pool = pool_bytes;
   }
-  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, 8 * sizeof(int)));
+  if (!b->d_count) GB_HIP(hipMalloc(&b->d_count, kCountWords * sizeof(int)));
   return GB_OK;
 }
 
@@ -1313,10 +1396,14 @@ int batch_fill(gb_phmm_batch *b, const gb_testcase *tcs, int n, int threads = 0,
   if (const char *e = getenv("GB_PHMM_RPL")) b->rpl = atoi(e) == 2 ? 2 : 1;
   b->w2 = 0;
   if (const char *e = getenv("GB_PHMM_W2")) b->w2 = atoi(e);
-  // two work units per stack in the f64 pass: the 1/8 shard's f64 pass 2.28 -> 2.00 ms, the whole job
-  // unchanged (13.62 -> 13.54 ms); four: no gain (profiles/r05e_phmm_f64_parts.log)
-  b->f64_parts = 2;
-  if (const char *e = getenv("GB_PHMM_F64_PARTS")) b->f64_parts = std::max(1, std::min(8, atoi(e)));
+  // work units per stack in the f64 pass: in stack order, two units per stack took the 1/8 shard's
+  // f64 pass 2.28 -> 2.00 ms (profiles/r05e_phmm_f64_parts.log); ordered by cost (f64_plan) one unit
+  // per stack is best: the shard 1.93 (stack order, two) -> 1.82 (plan, two) -> 1.78 ms (plan, one), the
+  // whole job 13.19 -> 13.07 -> 12.95 ms (profiles/r06x_phmm_f64_plan.log)
+  b->f64_parts = 1;
+  if (const char *e = getenv("GB_PHMM_F64_PARTS")) b->f64_parts = std::max(1, std::min(kMaxF64Parts, atoi(e)));
+  b->f64_plan = true;
+  if (const char *e = getenv("GB_PHMM_F64_PLAN")) b->f64_plan = atoi(e) != 0;
   // the f32 pass drops a testcase's remaining rows once its crossing mass proves it falls back to f64
   // (phmm_stack kExit): f32 pass 19.05 -> 18.40 ms, step +2.0 % (profiles/r05zzi_phmm_exit_ab.log);
   // finals, raw f64 and the fallback choice unchanged, a dropped testcase's raw f32 reads 0
@@ -1466,6 +1553,7 @@ int batch_new(DeviceTables *tabs, gb_phmm_batch **out) {
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, tabs->device) != hipSuccess) cus = 256;
   b->f64_grid = cus * 16;
+  if (const char *e = getenv("GB_PHMM_F64_GRID")) b->f64_grid = cus * std::max(1, std::min(32, atoi(e)));  // probe
   b->cus = cus;
   hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
   for (auto &ev : b->ev)
@@ -1651,7 +1739,7 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
   GB_HIP(hipSetDevice(t->device));
   const int n = b->n;
   GB_HIP(hipEventRecord(b->ev[0], b->stream));
-  GB_HIP(hipMemsetAsync(b->d_count, 0, 8 * sizeof(int), b->stream));
+  GB_HIP(hipMemsetAsync(b->d_count, 0, kCountWords * sizeof(int), b->stream));
   GB_HIP(hipMemsetAsync(b->d_rd, 0, sizeof(double) * std::max(n, 1), b->stream));
   if (n > 0) {
     const size_t rec = (size_t)(b->max_haplen + kBndPad + kRecPad), codes = (size_t)(b->max_haplen + kBndPad + kWave);
@@ -1672,26 +1760,37 @@ int gb_phmm_batch_run(gb_phmm_batch *b) {
       } else if (ns > 0) {
         hipLaunchKernelGGL(f32k, dim3(ns), dim3(kWave), lds_f, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
                            b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf, (const float *)nullptr,
-                           b->d_count, 0, (uint8_t *)nullptr, (size_t)0);
+                           b->d_count, 0, (uint8_t *)nullptr, (size_t)0, (const uint32_t *)nullptr);
       }
       if (nl > 0)
         hipLaunchKernelGGL((phmm_forward<float, false, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
                            nl, b->d_stk_tc, b->d_desc, b->d_pool, dev_tab<float>(t->f, t->hf.init_const), b->d_rf,
-                           (const float *)nullptr, b->d_count, 0, b->d_scratch, b->scratch_stride);
+                           (const float *)nullptr, b->d_count, 0, b->d_scratch, b->scratch_stride,
+                           (const uint32_t *)nullptr);
       GB_HIP(hipGetLastError());
     }
     GB_HIP(hipEventRecord(b->ev[1], b->stream));
     // f64 fallback: persistent grid over the stacks, each recomputing its flagged testcases
     if (ns > 0) {
-      const int g64 = std::min(ns * b->f64_parts, b->f64_grid);
+      const int nunits = ns * b->f64_parts;
+      const int g64 = std::min(nunits, b->f64_grid);
+      if (b->f64_plan) {
+        const dim3 pg((unsigned)((nunits + 255) / 256)), pb(256);
+        hipLaunchKernelGGL(f64_plan, pg, pb, 0, b->stream, b->d_stacks, nunits, b->f64_parts, b->d_stk_tc, b->d_desc,
+                           (const float *)b->d_rf, b->force_f64 ? 1 : 0, b->d_ukey, b->d_count);
+        hipLaunchKernelGGL(f64_plan_order, pg, pb, 0, b->stream, nunits, (const uint8_t *)b->d_ukey, b->d_count,
+                           b->d_units);
+      }
       hipLaunchKernelGGL(f64k, dim3(g64), dim3(kWave), lds_d, b->stream, b->d_stacks, ns, b->d_stk_tc, b->d_desc,
                          b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd, (const float *)b->d_rf,
-                         b->d_count, (b->force_f64 ? 1 : 0) | (b->f64_parts << 8), (uint8_t *)nullptr, (size_t)0);
+                         b->d_count, (b->force_f64 ? 1 : 0) | (b->f64_parts << 8), (uint8_t *)nullptr, (size_t)0,
+                         b->f64_plan ? (const uint32_t *)b->d_units : nullptr);
     }
     if (nl > 0)
       hipLaunchKernelGGL((phmm_forward<double, true, true>), dim3(b->long_grid), dim3(kWave), 0, b->stream, d_long,
                          nl, b->d_stk_tc, b->d_desc, b->d_pool, dev_tab<double>(t->d, t->hd.init_const), b->d_rd,
-                         (const float *)b->d_rf, b->d_count, b->force_f64 ? 1 : 0, b->d_scratch, b->scratch_stride);
+                         (const float *)b->d_rf, b->d_count, b->force_f64 ? 1 : 0, b->d_scratch, b->scratch_stride,
+                         (const uint32_t *)nullptr);
     GB_HIP(hipGetLastError());
     GB_HIP(hipEventRecord(b->ev[2], b->stream));
     hipLaunchKernelGGL(phmm_finalize, dim3((n + 255) / 256), dim3(256), 0, b->stream, b->d_rf,

@@ -306,3 +306,27 @@ def test_tail_split_stacks_exact(phmm, monkeypatch, tail):
     db.run()
     assert_exact(db.results()[:4], exp)
     db.close()
+
+
+@pytest.mark.parametrize("knobs", ["GB_PHMM_F64_PLAN=0", "GB_PHMM_F64_PARTS=2", "GB_PHMM_F64_PARTS=8",
+                                   "GB_PHMM_F64_PARTS=3,GB_PHMM_STACK_ROWS=512", "GB_PHMM_F64_PLAN=0,GB_PHMM_F64_PARTS=2"])
+def test_f64_plan_exact(phmm, monkeypatch, knobs):
+    """The f64 pass's units ordered by cost (csrc/phmm.hip f64_plan / f64_plan_order: only units with
+    fallback rows, costliest first; default one unit per stack) against stack order and several
+    units per stack -- bit-exact, the fallback count equal, repeated runs of one batch identical."""
+    for kv in knobs.split(","):
+        k, v = kv.split("=")
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(59)
+    ta = TestcaseArray.from_batches([gen.phmm_batch(rng, 50, 20) for _ in range(4)])
+    exp = oracle_run(ta)
+    nfb = int((exp[1] < 1e-28).sum())
+    assert nfb > 0
+    db = phmm.DeviceBatch(ta)
+    try:
+        for _ in range(2):
+            db.run()
+            assert_exact(db.results()[:4], exp)
+            assert db.stats()[2] == nfb
+    finally:
+        db.close()

@@ -58,6 +58,19 @@ constexpr int kIters = 4096;
 #define OP_MULF_DPP(r) asm volatile("v_mul_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define OP_MULF_ROR(r) asm volatile("v_mul_f32_dpp %0, %0, %1 wave_ror:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
 #define OP_ADDF_DPP(r) asm volatile("v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(k));
+#define OP_ADDCO(r) asm volatile("v_add_co_u32 %0, vcc, -1, %0" : "+v"(r) : : "vcc");
+#define OP_ADDC(r) asm volatile("v_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(r) : : "vcc");
+#define OP_CARRYPAIR(r) asm volatile("v_add_co_u32 %0, vcc, -1, %1\n v_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(r) : "v"(k) : "vcc");
+#define OP_MINSDWA(r) asm volatile("v_min_u32_sdwa %0, %1, 1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(k));
+#define OP_MOVSDWA(r) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0" : "+v"(r) : "v"(k));
+#define OP_ORSDWA(r) asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(k));
+#define OP_MULU24(r) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(r) : "v"(k));
+#define OP_MADU24(r) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+#define OP_MINU(r) asm volatile("v_min_u32 %0, %0, %1" : "+v"(r) : "v"(k));
+#define OP_SUBREV(r) asm volatile("v_subrev_u32 %0, %0, %1" : "+v"(r) : "v"(k));
+#define OP_ADD3(r) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+#define OP_OR3(r) asm volatile("v_or3_b32 %0, %0, %1, %1" : "+v"(r) : "v"(k));
+#define OP_BITOP3(r) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0xca" : "+v"(r) : "v"(k));
 #define OP_ADDF64(r) asm volatile("v_add_f64 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
 #define OP_MULF64(r) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
 #define OP_PKADDF(r) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(*(double *)&r) : "v"(*(double *)&k));
@@ -95,6 +108,19 @@ KERNEL(k_cmp, OP_CMP, 1u)
 KERNEL(k_mulf_dpp, OP_MULF_DPP, 0x3f800000u)
 KERNEL(k_mulf_ror, OP_MULF_ROR, 0x3f800000u)
 KERNEL(k_addf_dpp, OP_ADDF_DPP, 0x3f800000u)
+KERNEL(k_addco, OP_ADDCO, 1u)
+KERNEL(k_addc, OP_ADDC, 1u)
+KERNEL(k_carrypair, OP_CARRYPAIR, 1u)
+KERNEL(k_minsdwa, OP_MINSDWA, 1u)
+KERNEL(k_movsdwa, OP_MOVSDWA, 1u)
+KERNEL(k_orsdwa, OP_ORSDWA, 1u)
+KERNEL(k_mulu24, OP_MULU24, 3u)
+KERNEL(k_madu24, OP_MADU24, 3u)
+KERNEL(k_minu, OP_MINU, 1u)
+KERNEL(k_subrev, OP_SUBREV, 1u)
+KERNEL(k_add3, OP_ADD3, 1u)
+KERNEL(k_or3, OP_OR3, 1u)
+KERNEL(k_bitop3, OP_BITOP3, 1u)
 
 #define KERNEL64(NAME, OP)                                                                          \
   __global__ __launch_bounds__(256) void NAME(uint32_t *out, unsigned long long *clk, uint32_t s) {  \
@@ -138,6 +164,10 @@ int main() {
       {"v_max_f32", k_maxf}, {"v_add_u16", k_addi16}, {"v_lshl_or_b32", k_lshlor},
       {"cmp+cndmask(vcc)x2", k_cmpcnd}, {"cndmask(sgpr)", k_cnds}, {"v_cmp(vcc)", k_cmp},
       {"v_mul_f32_dpp row_shr", k_mulf_dpp}, {"v_mul_f32_dpp wave_ror", k_mulf_ror}, {"v_add_f32_dpp row_shr", k_addf_dpp},
+      {"v_add_co_u32(vcc)", k_addco}, {"v_addc_co_u32(vcc)", k_addc}, {"add_co+addc pair x2", k_carrypair},
+      {"v_min_u32_sdwa byte", k_minsdwa}, {"v_mov_b32_sdwa word", k_movsdwa}, {"v_or_b32_sdwa byte", k_orsdwa},
+      {"v_mul_u32_u24", k_mulu24}, {"v_mad_u32_u24", k_madu24}, {"v_min_u32", k_minu}, {"v_subrev_u32", k_subrev},
+      {"v_add3_u32", k_add3}, {"v_or3_b32", k_or3}, {"v_bitop3_b32", k_bitop3},
       {"v_add_f64", k_addf64}, {"v_mul_f64", k_mulf64}, {"v_fma_f64", k_fmaf64}, {"v_pk_mul_f32", k_pkmulf},
       {"v_pk_add_f32", k_pkaddf}, {"v_pk_fma_f32", k_pkfmaf}};
   for (auto &k : ks) {
