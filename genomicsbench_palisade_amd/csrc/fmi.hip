@@ -62,6 +62,37 @@ __global__ void pack_q4(const uint8_t *__restrict__ qdb, int32_t stride, int32_t
   q4[r * q4_stride + w] = v;
 }
 
+// byte codes -> 2-bit codes, 16 per word (base b of word w at bits 2*(b); an N or any code >= 4 reads
+// 0 here), and per read its N positions: up to four, one per byte ascending, 0xFF = none
+// (kNOverflow: more than four, the search then reads that read's codes from qdb)
+constexpr uint32_t kNOverflow = 0xFEFEFEFEu;
+__global__ void pack_q2(const uint8_t *__restrict__ qdb, int32_t stride, int32_t nreads, int32_t q2_stride,
+                        uint32_t *__restrict__ q2) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = t / q2_stride, w = t % q2_stride;
+  if (r >= nreads) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 16; b++) {
+    const int64_t j = w * 16 + b;
+    const uint32_t c = j < stride ? (uint32_t)qdb[r * stride + j] : 0u;
+    v |= (c < 4 ? c : 0u) << (2 * b);
+  }
+  q2[r * q2_stride + w] = v;
+}
+__global__ void pack_npos(const uint8_t *__restrict__ qdb, int32_t stride, const int32_t *__restrict__ lens,
+                          int32_t nreads, uint32_t *__restrict__ npos) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nreads) return;
+  uint32_t v = 0xFFFFFFFFu;
+  int n = 0;
+  for (int j = 0; j < lens[r]; j++)
+    if (qdb[r * stride + j] >= 4) {
+      if (n < 4) v = (v & ~(0xFFu << (8 * n))) | ((uint32_t)j << (8 * n));
+      n++;
+    }
+  npos[r] = n > 4 ? kNOverflow : v;
+}
+
 // CP_OCC (one-hot planes, MSB = first row) -> Occ32 (2-bit codes, LSB = first row), one per block
 __global__ void compress_occ(const CpOcc *__restrict__ occ, int64_t cp_size, Occ32 *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -104,6 +135,9 @@ struct SearchArgs {
   const uint8_t *qdb;
   const uint32_t *q4;    // nibble-packed copy of qdb (8 bases per word), q4_stride words per read
   int32_t q4_stride;
+  const uint32_t *q2;    // 2-bit copy of qdb (16 bases per word), q2_stride words per read (pack_q2)
+  int32_t q2_stride;
+  const uint32_t *npos;  // per read: its N positions (pack_npos)
   const int32_t *lens;
   int32_t nreads, stride, min_seed_len, split_len;
   PEnt *scratch;         // per wave: stride x 64 entries, wave-interleaved
@@ -168,6 +202,12 @@ __device__ void heap_sort(gb_smem *a, int n) {
 constexpr int kQBases = 152;
 constexpr int kQW = kQBases / 8;
 static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
+// kQ 2: the same reads staged at 2 bits per base (11 words per lane row, odd; 2.75 KB per wave
+// instead of 4.75) with the read's N positions in one register (pack_npos): the 2 KB saved hold two
+// more `prev` head entries at the same 16 waves per CU. A read with more than four N's reads its
+// bases from qdb instead.
+constexpr int kQW2 = 11;
+static_assert(kQW2 * 16 >= kQBases && kQW2 % 2 == 1, "2-bit rows: every base, odd stride");
 
 // kTop: the first entries of every `prev` list (list indices p < kTop, where the backward loop's
 // reads and its in-place compaction concentrate as the lists shrink) live in LDS, the rest in the
@@ -185,10 +225,12 @@ __device__ __forceinline__ int ring_slot(int x) {
     return (int)((unsigned)x % (unsigned)N);
 }
 
-template <bool kLdsQ, int kTop>  // kTop 0: every entry in the scratch
+template <int kQ, int kTop>  // kQ: read codes 0 from qdb, 1 staged 4-bit, 2 staged 2-bit; kTop 0: every entry in the scratch
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   constexpr bool kTopLds = kTop > 0;
-  __shared__ uint32_t Qs[kLdsQ ? 64 * kQW : 1];
+  constexpr bool kLdsQ = kQ > 0;
+  constexpr int kRowW = kQ == 2 ? kQW2 : kQW;
+  __shared__ uint32_t Qs[kLdsQ ? 64 * kRowW : 1];
   __shared__ PEnt Ltop[kTopLds ? kTop * 64 : 1];
   const DevIndex F = A.F;
   const int gid = blockIdx.x * 64 + threadIdx.x;
@@ -201,12 +243,19 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   int st = NEXT_READ;
   int rd = 0, L = 0, mode = 0, nslot = -1;
   const uint8_t *q = nullptr;
-  uint32_t *const qrow = Qs + (kLdsQ ? threadIdx.x * kQW : 0);
+  uint32_t *const qrow = Qs + (kLdsQ ? threadIdx.x * kRowW : 0);
+  uint32_t nw = 0xFFFFFFFFu;  // kQ 2: the read's N positions (pack_npos)
   auto base_at = [&](int idx) -> int {
-    if constexpr (kLdsQ)
+    if constexpr (kQ == 2) {
+      const int c = (int)((qrow[idx >> 4] >> (2 * (idx & 15))) & 3u);
+      // idx is an N position iff some byte of nw ^ (idx in every byte) is zero
+      const uint32_t x = nw ^ __builtin_amdgcn_perm(0u, (uint32_t)idx, 0u);
+      return ((x - 0x01010101u) & ~x & 0x80808080u) ? 4 : c;
+    } else if constexpr (kQ == 1) {
       return (int)((qrow[idx >> 3] >> (4 * (idx & 7))) & 15u);
-    else
+    } else {
       return q[idx];
+    }
   };
   gb_smem *o = nullptr;
   int nout = 0, n1 = 0, n2 = 0, ridx = 0;
@@ -327,7 +376,27 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           rd = A.list ? A.list[slot] : slot;
           L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
-          if constexpr (kLdsQ) {
+          if constexpr (kQ == 2) {
+            nw = A.npos[rd];
+            if (nw == kNOverflow) {
+              // more than four N's: the read goes to smem_heavy (which reads qdb) before it starts,
+              // so the lookups here need no byte-load path
+              const int h = atomicAdd(A.heavy_n, 1);
+              A.heavy[2 * h] = rd;
+              A.heavy[2 * h + 1] = -1;
+              break;  // st stays NEXT_READ
+            }
+            // rows are q2_stride (a multiple of 4) words: all 16-byte loads issue together
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.q2 + (size_t)rd * A.q2_stride);
+            const int n4 = (L + 63) >> 6;
+            for (int w = 0; w < n4; w++) {
+              const uint4 v = src[w];
+              if (4 * w < kQW2) qrow[4 * w] = v.x;
+              if (4 * w + 1 < kQW2) qrow[4 * w + 1] = v.y;
+              if (4 * w + 2 < kQW2) qrow[4 * w + 2] = v.z;
+              if (4 * w + 3 < kQW2) qrow[4 * w + 3] = v.w;
+            }
+          } else if constexpr (kQ == 1) {
             // rows are q4_stride (a multiple of 4) words: all 16-byte loads issue together
             const uint4 *src = reinterpret_cast<const uint4 *>(A.q4 + (size_t)rd * A.q4_stride);
             const int n4 = (L + 31) >> 5;
@@ -898,6 +967,9 @@ struct gb_fmi_reads {
   uint8_t *d_qdb = nullptr;
   uint32_t *d_q4 = nullptr;
   int32_t q4_stride = 0;
+  uint32_t *d_q2 = nullptr;    // 2-bit codes (smem_search<2, ...>)
+  int32_t q2_stride = 0;
+  uint32_t *d_npos = nullptr;  // per read: N positions
   int32_t *d_lens = nullptr;
   gbfmi::PEnt *d_scratch = nullptr;
   gb_smem *d_slots = nullptr;
@@ -924,6 +996,7 @@ struct gb_fmi_reads {
   // grow-only capacities (bytes): a destroyed read set goes back to its thread's free list with its
   // stream and buffers, and the next create reuses them (no hipMalloc / hipFree per batch)
   int device = -1;
+  size_t cap_q2 = 0, cap_npos = 0;
   size_t cap_qdb = 0, cap_q4 = 0, cap_lens = 0, cap_scratch = 0, cap_slots = 0, cap_ovf_pos = 0, cap_counts = 0,
          cap_phase = 0, cap_offsets = 0, cap_temp = 0, cap_heavy = 0;
 };
@@ -938,17 +1011,30 @@ int device_cus() {
   return cus;
 }
 
-// `prev` list head entries kept in LDS (GB_FMI_TOP: 0, 4-8). Five (9.9 KB per wave with the staged
-// read codes, 16 waves per CU still fit): 10 M reads 243.9 -> 232.7 ms, the 1/8 shard 35.2 -> 34.0 ms
-// against four; six at 14 / 15 waves 233.8, seven at 13 249.7, eight at 11 259.6
-// (profiles/r05zi_fmi_top.log)
+// read codes staged at 2 bits per base (smem_search<2, ...>; GB_FMI_Q2=0: 4 bits, the round-5 form)
+bool q2_codes() {
+  const char *e = getenv("GB_FMI_Q2");
+  return !(e && *e == '0');
+}
+
+// `prev` list head entries kept in LDS (GB_FMI_TOP: 0, 4-8). With 4-bit codes five (9.9 KB per wave,
+// 16 waves per CU still fit): 10 M reads 243.9 -> 232.7 ms, the 1/8 shard 35.2 -> 34.0 ms against
+// four; six at 14 / 15 waves 233.8, seven at 13 249.7, eight at 11 259.6 (profiles/r05zi_fmi_top.log).
+// With 2-bit codes (2.75 KB) seven fit at 16 waves (9.75 KB, five 2-KB granules).
 int top_entries() {
   const char *te = getenv("GB_FMI_TOP");
-  return te ? atoi(te) : 5;
+  return te ? atoi(te) : (q2_codes() ? 7 : 5);
 }
 
 int lanes_for_device(int cus) {
   const char *e = getenv("GB_FMI_WAVES_PER_CU");
+  if (q2_codes() && !e) {
+    // 2-bit codes: LDS per wave 2 816 B + 1 KB per head entry, allocated in 2 KB granules; 16 waves
+    // per CU at most (116 VGPRs)
+    const int lds = 64 * 4 * gbfmi::kQW2 + 1024 * top_entries();
+    const int gran = (lds + 2047) / 2048 * 2048;
+    return cus * std::max(1, std::min(16, 160 * 1024 / gran)) * 64;
+  }
   // Waves (workgroups) per CU of the persistent grid. LDS per wave is the staged read codes (4.9 KB)
   // plus the `prev` list head (1 KB per entry kept); 116 VGPRs allow 4 waves per SIMD. With an
   // 8-entry head (13 KB) 12 fit and 11 / 12 run alike; a 4- or 5-entry head (8.9 / 9.9 KB) lets the
@@ -1266,14 +1352,22 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
   if (e == hipSuccess && num_reads) e = gb::memcpy_big(R->d_qdb, enc_qdb, (size_t)num_reads * max_readlength, hipMemcpyHostToDevice);
   R->q4_stride = (((max_readlength + 7) / 8) + 3) & ~3;  // 16-byte rows (smem_search staging)
   reserve(&R->d_q4, &R->cap_q4, nr * (size_t)R->q4_stride * sizeof(uint32_t));
+  R->q2_stride = (((max_readlength + 15) / 16) + 3) & ~3;
+  reserve(&R->d_q2, &R->cap_q2, nr * (size_t)R->q2_stride * sizeof(uint32_t));
+  reserve(&R->d_npos, &R->cap_npos, nr * sizeof(uint32_t));
+  if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_lens, lens, (size_t)num_reads * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e == hipSuccess && num_reads) {
     const int64_t nt = (int64_t)num_reads * R->q4_stride;
     hipLaunchKernelGGL(gbfmi::pack_q4, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
                        max_readlength, num_reads, R->q4_stride, R->d_q4);
+    const int64_t n2 = (int64_t)num_reads * R->q2_stride;
+    hipLaunchKernelGGL(gbfmi::pack_q2, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
+                       max_readlength, num_reads, R->q2_stride, R->d_q2);
+    hipLaunchKernelGGL(gbfmi::pack_npos, dim3((unsigned)((num_reads + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
+                       max_readlength, R->d_lens, num_reads, R->d_npos);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(R->stream);
   }
-  if (e == hipSuccess && num_reads) e = hipMemcpy(R->d_lens, lens, (size_t)num_reads * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     gb::set_error("gb_fmi_reads_create: %s", hipGetErrorString(e));
     R->complete = false;  // a partly built read set is freed, never recycled
@@ -1294,7 +1388,7 @@ int gb_fmi_reads_destroy(gb_fmi_reads *R) {
     free_reads().push_back(R);
     return GB_OK;
   }
-  for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
+  for (void *p : {(void *)R->d_qdb, (void *)R->d_q4, (void *)R->d_q2, (void *)R->d_npos, (void *)R->d_lens, (void *)R->d_scratch, (void *)R->d_slots,
                   (void *)R->d_counts, (void *)R->d_phase, (void *)R->d_offsets, (void *)R->d_out,
                   (void *)R->d_ctl, (void *)R->d_calls, R->d_temp, (void *)R->d_ovf_list,
                   (void *)R->d_ovf_pos, (void *)R->d_big, (void *)R->d_trace, (void *)R->d_heavy})
@@ -1322,6 +1416,9 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
   A.qdb = R->d_qdb;
   A.q4 = R->d_q4;
   A.q4_stride = R->q4_stride;
+  A.q2 = R->d_q2;
+  A.q2_stride = R->q2_stride;
+  A.npos = R->d_npos;
   A.lens = R->d_lens;
   A.nreads = R->nreads;
   A.stride = R->stride;
@@ -1374,26 +1471,38 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     const int top = top_entries();
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, R->stream, A); };
     const char *qe = getenv("GB_FMI_QLDS");  // 0: read codes from global memory, not staged in LDS
-    if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0')) {
+    // the 2-bit form hands reads with more than four N's to the heavy pass, so it needs that pass
+    if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0') && q2_codes() && A.budget != INT32_MAX) {
       if (top >= 8)
-        launch(gbfmi::smem_search<true, 8>);
+        launch(gbfmi::smem_search<2, 8>);
       else if (top >= 7)
-        launch(gbfmi::smem_search<true, 7>);
+        launch(gbfmi::smem_search<2, 7>);
       else if (top >= 6)
-        launch(gbfmi::smem_search<true, 6>);
+        launch(gbfmi::smem_search<2, 6>);
       else if (top >= 5)
-        launch(gbfmi::smem_search<true, 5>);
-      else if (top >= 4)
-        launch(gbfmi::smem_search<true, 4>);
+        launch(gbfmi::smem_search<2, 5>);
       else
-        launch(gbfmi::smem_search<true, 0>);
+        launch(gbfmi::smem_search<2, 0>);
+    } else if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0')) {
+      if (top >= 8)
+        launch(gbfmi::smem_search<1, 8>);
+      else if (top >= 7)
+        launch(gbfmi::smem_search<1, 7>);
+      else if (top >= 6)
+        launch(gbfmi::smem_search<1, 6>);
+      else if (top >= 5)
+        launch(gbfmi::smem_search<1, 5>);
+      else if (top >= 4)
+        launch(gbfmi::smem_search<1, 4>);
+      else
+        launch(gbfmi::smem_search<1, 0>);
     } else {
       if (top >= 8)
-        launch(gbfmi::smem_search<false, 8>);
+        launch(gbfmi::smem_search<0, 8>);
       else if (top >= 4)
-        launch(gbfmi::smem_search<false, 4>);
+        launch(gbfmi::smem_search<0, 4>);
       else
-        launch(gbfmi::smem_search<false, 0>);
+        launch(gbfmi::smem_search<0, 0>);
     }
     GB_HIP(hipGetLastError());
     if (A.budget != INT32_MAX) {

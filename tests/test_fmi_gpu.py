@@ -97,6 +97,34 @@ def test_prev_head_sizes_exact(fmi, monkeypatch, top):
     assert rs.timing()[2] == oi.bwt_calls()
 
 
+@pytest.mark.parametrize("q2,n_rate", [("1", 0.002), ("1", 0.03), ("1", 0.2), ("0", 0.03)])
+def test_read_code_staging_exact(fmi, monkeypatch, q2, n_rate):
+    """The search's read codes staged at 2 bits per base with each read's N positions in a register
+    (GB_FMI_Q2=1, default; pack_q2 / pack_npos; a read with more than four N's reads its bases from
+    qdb) or at 4 bits (GB_FMI_Q2=0), on reads from no N to mostly N's, a quarter of them in a
+    repeat-rich reference, ragged lengths included: SMEMs, counts and backwardExt calls equal the
+    oracle's."""
+    monkeypatch.setenv("GB_FMI_Q2", q2)
+    ref = gen.fmi_reference(300_000, seed=43, repeat_frac=0.25)
+    codes, lens = gen.fmi_reads(ref, 2500, read_len=151, seed=44, sub_rate=0.03, n_rate=n_rate)
+    lens = lens.copy()
+    lens[::89] = np.maximum(1, lens[::89] // 2)
+    nper = [(codes[r, :lens[r]] >= 4).sum() for r in range(len(lens))]
+    if n_rate == 0.03:
+        assert max(nper) > 4 and min(nper) <= 4  # both the register and the qdb form
+    elif n_rate == 0.2:
+        assert min(nper) > 4  # every read through qdb
+    oi = fmi_util.OracleIndex(ref)
+    exp, ebc, epc = oi.run(codes, lens, batch_size=512)
+    idx = fmi.Index.build(ref)
+    rs = fmi.Reads(idx, codes, lens)
+    rs.search(19)
+    sm, tot, bc, pc = rs.results(batch_size=512)
+    assert tot == len(exp) and (bc == ebc).all() and (pc == epc).all()
+    assert (smem_tuple_array(sm) == smem_tuple_array(exp)).all()
+    assert rs.timing()[2] == oi.bwt_calls()
+
+
 def test_search_repeat_runs_identical(fmi):
     ref = gen.fmi_reference(100_000, seed=9)
     codes, lens = gen.fmi_reads(ref, 1500, seed=10)

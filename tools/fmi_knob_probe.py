@@ -14,7 +14,7 @@ if os.environ.get("FMI_LIB"):  # another build of libgb.so, to time two builds o
     g.LIBGB = os.path.abspath(os.environ["FMI_LIB"])
 from genomicsbench_palisade_amd import fmi, gen, set_device, shard  # noqa: E402
 
-KNOBS = ("GB_FMI_WAVES_PER_CU", "GB_FMI_TOP", "GB_FMI_HEAVY", "GB_FMI_QLDS", "GB_FMI_PREFETCH", "GB_FMI_SPLIT")
+KNOBS = ("GB_FMI_WAVES_PER_CU", "GB_FMI_TOP", "GB_FMI_HEAVY", "GB_FMI_QLDS", "GB_FMI_PREFETCH", "GB_FMI_SPLIT", "GB_FMI_Q2")
 set_device(0)
 nreads = int(os.environ.get("FMI_PROBE_READS", "10000000"))
 ref = gen.fmi_reference(512_000_000, seed=7)
