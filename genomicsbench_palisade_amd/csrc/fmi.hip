@@ -374,7 +374,6 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           // but a claimed read waits behind the current one, which lengthens the grid's tail
           if (A.prefetch) nslot = atomicAdd(A.next_read, 1);
           rd = A.list ? A.list[slot] : slot;
-          L = A.lens[rd];
           q = A.qdb + (size_t)rd * A.stride;
           if constexpr (kQ == 2) {
             nw = A.npos[rd];
@@ -386,6 +385,12 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
               A.heavy[2 * h + 1] = -1;
               break;  // st stays NEXT_READ
             }
+          }
+          // L is loaded after that branch: loaded before it, the hand-over path left the load
+          // outstanding as far as the compiler's wait analysis could tell, and every later use of L
+          // in the state machine got a vmcnt(0) wait -- which also waited for the trip's stores
+          L = A.lens[rd];
+          if constexpr (kQ == 2) {
             // rows are q2_stride (a multiple of 4) words: all 16-byte loads issue together
             const uint4 *src = reinterpret_cast<const uint4 *>(A.q2 + (size_t)rd * A.q2_stride);
             const int n4 = (L + 63) >> 6;
