@@ -63,34 +63,33 @@ __global__ void pack_q4(const uint8_t *__restrict__ qdb, int32_t stride, int32_t
 }
 
 // byte codes -> 2-bit codes, 16 per word (base b of word w at bits 2*(b); an N or any code >= 4 reads
-// 0 here), and per read its N positions: up to four, one per byte ascending, 0xFF = none
-// (kNOverflow: more than four, the search then reads that read's codes from qdb)
+// 0 here), and per read its N positions: up to four, one per byte (in any order: the search only
+// tests membership), 0xFF = none (kNOverflow: more than four; the search hands such a read to the
+// heavy pass). npos starts all ones and ncnt zero; an N (rare) takes a byte by an atomic count and
+// writes it with one atomic AND; npos_finish marks the reads with more than four.
 constexpr uint32_t kNOverflow = 0xFEFEFEFEu;
-__global__ void pack_q2(const uint8_t *__restrict__ qdb, int32_t stride, int32_t nreads, int32_t q2_stride,
-                        uint32_t *__restrict__ q2) {
+__global__ void pack_q2(const uint8_t *__restrict__ qdb, int32_t stride, const int32_t *__restrict__ lens,
+                        int32_t nreads, int32_t q2_stride, uint32_t *__restrict__ q2, uint32_t *__restrict__ npos,
+                        int32_t *__restrict__ ncnt) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t r = t / q2_stride, w = t % q2_stride;
   if (r >= nreads) return;
+  const int L = lens[r];
   uint32_t v = 0;
   for (int b = 0; b < 16; b++) {
     const int64_t j = w * 16 + b;
     const uint32_t c = j < stride ? (uint32_t)qdb[r * stride + j] : 0u;
     v |= (c < 4 ? c : 0u) << (2 * b);
+    if (c >= 4 && j < L) {
+      const int k = atomicAdd(&ncnt[r], 1);
+      if (k < 4) atomicAnd(&npos[r], ~(0xFFu << (8 * k)) | ((uint32_t)j << (8 * k)));
+    }
   }
   q2[r * q2_stride + w] = v;
 }
-__global__ void pack_npos(const uint8_t *__restrict__ qdb, int32_t stride, const int32_t *__restrict__ lens,
-                          int32_t nreads, uint32_t *__restrict__ npos) {
+__global__ void npos_finish(const int32_t *__restrict__ ncnt, int32_t nreads, uint32_t *__restrict__ npos) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nreads) return;
-  uint32_t v = 0xFFFFFFFFu;
-  int n = 0;
-  for (int j = 0; j < lens[r]; j++)
-    if (qdb[r * stride + j] >= 4) {
-      if (n < 4) v = (v & ~(0xFFu << (8 * n))) | ((uint32_t)j << (8 * n));
-      n++;
-    }
-  npos[r] = n > 4 ? kNOverflow : v;
+  if (r < nreads && ncnt[r] > 4) npos[r] = kNOverflow;
 }
 
 // CP_OCC (one-hot planes, MSB = first row) -> Occ32 (2-bit codes, LSB = first row), one per block
@@ -1365,12 +1364,15 @@ int gb_fmi_reads_create(gb_fmi_index *idx, const uint8_t *enc_qdb, const int32_t
     const int64_t nt = (int64_t)num_reads * R->q4_stride;
     hipLaunchKernelGGL(gbfmi::pack_q4, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
                        max_readlength, num_reads, R->q4_stride, R->d_q4);
+    // N positions: npos all ones, the per-read N counts (d_counts, which the search rewrites) zero
+    e = hipMemsetAsync(R->d_npos, 0xFF, (size_t)num_reads * sizeof(uint32_t), R->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(R->d_counts, 0, (size_t)num_reads * sizeof(int32_t), R->stream);
     const int64_t n2 = (int64_t)num_reads * R->q2_stride;
     hipLaunchKernelGGL(gbfmi::pack_q2, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
-                       max_readlength, num_reads, R->q2_stride, R->d_q2);
-    hipLaunchKernelGGL(gbfmi::pack_npos, dim3((unsigned)((num_reads + 255) / 256)), dim3(256), 0, R->stream, R->d_qdb,
-                       max_readlength, R->d_lens, num_reads, R->d_npos);
-    e = hipGetLastError();
+                       max_readlength, R->d_lens, num_reads, R->q2_stride, R->d_q2, R->d_npos, R->d_counts);
+    hipLaunchKernelGGL(gbfmi::npos_finish, dim3((unsigned)((num_reads + 255) / 256)), dim3(256), 0, R->stream,
+                       R->d_counts, num_reads, R->d_npos);
+    if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(R->stream);
   }
   if (e != hipSuccess) {
