@@ -207,6 +207,11 @@ static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
 // bases from qdb instead.
 constexpr int kQW2 = 11;
 static_assert(kQW2 * 16 >= kQBases && kQW2 % 2 == 1, "2-bit rows: every base, odd stride");
+// kQ 3 (default): the first 128 bases' 2-bit codes in LDS (8 words, 2 KB per wave) and bases
+// 128..159 in two registers, so eight head entries fit 16 waves per CU (10 KB). (64 bases in LDS and
+// six registers for nine entries pushed the kernel past 128 VGPRs into scratch spills: 382 ms.)
+constexpr int kQW3 = 8;
+static_assert(kQW3 * 16 + 32 >= kQBases, "2-bit split rows: every base");
 
 // kTop: the first entries of every `prev` list (list indices p < kTop, where the backward loop's
 // reads and its in-place compaction concentrate as the lists shrink) live in LDS, the rest in the
@@ -228,7 +233,7 @@ template <int kQ, int kTop>  // kQ: read codes 0 from qdb, 1 staged 4-bit, 2 sta
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   constexpr bool kTopLds = kTop > 0;
   constexpr bool kLdsQ = kQ > 0;
-  constexpr int kRowW = kQ == 2 ? kQW2 : kQW;
+  constexpr int kRowW = kQ == 3 ? kQW3 : kQ == 2 ? kQW2 : kQW;
   __shared__ uint32_t Qs[kLdsQ ? 64 * kRowW : 1];
   __shared__ PEnt Ltop[kTopLds ? kTop * 64 : 1];
   const DevIndex F = A.F;
@@ -243,10 +248,18 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   int rd = 0, L = 0, mode = 0, nslot = -1;
   const uint8_t *q = nullptr;
   uint32_t *const qrow = Qs + (kLdsQ ? threadIdx.x * kRowW : 0);
-  uint32_t nw = 0xFFFFFFFFu;  // kQ 2: the read's N positions (pack_npos)
+  uint32_t nw = 0xFFFFFFFFu;  // kQ 2 / 3: the read's N positions (pack_q2)
+  uint32_t qh0 = 0, qh1 = 0;  // kQ 3: the code words of bases 128..143 and 144..159
   auto base_at = [&](int idx) -> int {
-    if constexpr (kQ == 2) {
-      const int c = (int)((qrow[idx >> 4] >> (2 * (idx & 15))) & 3u);
+    if constexpr (kQ >= 2) {
+      uint32_t w;
+      if constexpr (kQ >= 3) {
+        const uint32_t lw = qrow[min(idx >> 4, kRowW - 1)];
+        w = idx < 16 * kQW3 ? lw : (idx < 16 * kQW3 + 16 ? qh0 : qh1);
+      } else {
+        w = qrow[idx >> 4];
+      }
+      const int c = (int)((w >> (2 * (idx & 15))) & 3u);
       // idx is an N position iff some byte of nw ^ (idx in every byte) is zero
       const uint32_t x = nw ^ __builtin_amdgcn_perm(0u, (uint32_t)idx, 0u);
       return ((x - 0x01010101u) & ~x & 0x80808080u) ? 4 : c;
@@ -374,7 +387,7 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           if (A.prefetch) nslot = atomicAdd(A.next_read, 1);
           rd = A.list ? A.list[slot] : slot;
           q = A.qdb + (size_t)rd * A.stride;
-          if constexpr (kQ == 2) {
+          if constexpr (kQ >= 2) {
             nw = A.npos[rd];
             if (nw == kNOverflow) {
               // more than four N's: the read goes to smem_heavy (which reads qdb) before it starts,
@@ -389,7 +402,25 @@ __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
           // outstanding as far as the compiler's wait analysis could tell, and every later use of L
           // in the state machine got a vmcnt(0) wait -- which also waited for the trip's stores
           L = A.lens[rd];
-          if constexpr (kQ == 2) {
+          if constexpr (kQ >= 3) {
+            // words 0..7 to the LDS row, 8 and 9 to registers (q2_stride covers every word of the
+            // longest read; a word past the read is never looked at)
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.q2 + (size_t)rd * A.q2_stride);
+            const int n4 = (L + 63) >> 6;
+            const uint4 v0 = src[0];
+            const uint4 v1 = n4 > 1 ? src[1] : make_uint4(0, 0, 0, 0);
+            const uint4 v2 = n4 > 2 ? src[2] : make_uint4(0, 0, 0, 0);
+            qrow[0] = v0.x;
+            qrow[1] = v0.y;
+            qrow[2] = v0.z;
+            qrow[3] = v0.w;
+            qrow[4] = v1.x;
+            qrow[5] = v1.y;
+            qrow[6] = v1.z;
+            qrow[7] = v1.w;
+            qh0 = v2.x;
+            qh1 = v2.y;
+          } else if constexpr (kQ == 2) {
             // rows are q2_stride (a multiple of 4) words: all 16-byte loads issue together
             const uint4 *src = reinterpret_cast<const uint4 *>(A.q2 + (size_t)rd * A.q2_stride);
             const int n4 = (L + 63) >> 6;
@@ -1015,19 +1046,25 @@ int device_cus() {
   return cus;
 }
 
-// read codes staged at 2 bits per base (smem_search<2, ...>; GB_FMI_Q2=0: 4 bits, the round-5 form)
+// read codes staged at 2 bits per base: by default the split rows of smem_search<3, ...>
+// (GB_FMI_Q2=3); GB_FMI_Q2=1: whole 11-word rows (smem_search<2, ...>); 0: 4 bits, the round-5 form
 bool q2_codes() {
   const char *e = getenv("GB_FMI_Q2");
   return !(e && *e == '0');
+}
+bool q3_codes() {
+  const char *e = getenv("GB_FMI_Q2");
+  return !e || !*e || *e == '3';
 }
 
 // `prev` list head entries kept in LDS (GB_FMI_TOP: 0, 4-8). With 4-bit codes five (9.9 KB per wave,
 // 16 waves per CU still fit): 10 M reads 243.9 -> 232.7 ms, the 1/8 shard 35.2 -> 34.0 ms against
 // four; six at 14 / 15 waves 233.8, seven at 13 249.7, eight at 11 259.6 (profiles/r05zi_fmi_top.log).
-// With 2-bit codes (2.75 KB) seven fit at 16 waves (9.75 KB, five 2-KB granules).
+// With 2-bit codes (2.75 KB) seven fit at 16 waves (9.75 KB, five 2-KB granules); with the split rows
+// (2 KB) eight (10 KB): 10 M reads 227.3 -> 222.0 ms (profiles/r06zt_fmi_split_rows_ab.log).
 int top_entries() {
   const char *te = getenv("GB_FMI_TOP");
-  return te ? atoi(te) : (q2_codes() ? 7 : 5);
+  return te ? atoi(te) : (q3_codes() ? 8 : q2_codes() ? 7 : 5);
 }
 
 int lanes_for_device(int cus) {
@@ -1035,7 +1072,7 @@ int lanes_for_device(int cus) {
   if (q2_codes() && !e) {
     // 2-bit codes: LDS per wave 2 816 B + 1 KB per head entry, allocated in 2 KB granules; 16 waves
     // per CU at most (116 VGPRs)
-    const int lds = 64 * 4 * gbfmi::kQW2 + 1024 * top_entries();
+    const int lds = 64 * 4 * (q3_codes() ? gbfmi::kQW3 : gbfmi::kQW2) + 1024 * top_entries();
     const int gran = (lds + 2047) / 2048 * 2048;
     return cus * std::max(1, std::min(16, 160 * 1024 / gran)) * 64;
   }
@@ -1479,7 +1516,12 @@ int gb_fmi_search(gb_fmi_reads *R, int32_t min_seed_len) {
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, R->stream, A); };
     const char *qe = getenv("GB_FMI_QLDS");  // 0: read codes from global memory, not staged in LDS
     // the 2-bit form hands reads with more than four N's to the heavy pass, so it needs that pass
-    if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0') && q2_codes() && A.budget != INT32_MAX) {
+    if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0') && q3_codes() && A.budget != INT32_MAX) {
+      if (top >= 8)
+        launch(gbfmi::smem_search<3, 8>);
+      else
+        launch(gbfmi::smem_search<3, 7>);
+    } else if (R->stride <= gbfmi::kQBases && !(qe && *qe == '0') && q2_codes() && A.budget != INT32_MAX) {
       if (top >= 8)
         launch(gbfmi::smem_search<2, 8>);
       else if (top >= 7)

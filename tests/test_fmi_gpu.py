@@ -97,11 +97,11 @@ def test_prev_head_sizes_exact(fmi, monkeypatch, top):
     assert rs.timing()[2] == oi.bwt_calls()
 
 
-@pytest.mark.parametrize("q2,n_rate", [("1", 0.002), ("1", 0.03), ("1", 0.2), ("0", 0.03)])
+@pytest.mark.parametrize("q2,n_rate", [("3", 0.002), ("3", 0.03), ("3", 0.2), ("1", 0.03), ("1", 0.2), ("0", 0.03)])
 def test_read_code_staging_exact(fmi, monkeypatch, q2, n_rate):
     """The search's read codes staged at 2 bits per base with each read's N positions in a register
-    (GB_FMI_Q2=1, default; pack_q2 / pack_npos; a read with more than four N's reads its bases from
-    qdb) or at 4 bits (GB_FMI_Q2=0), on reads from no N to mostly N's, a quarter of them in a
+    (pack_q2; a read with more than four N's goes to the heavy pass) -- the first 128 bases in LDS and
+    the rest in registers (GB_FMI_Q2=3, default) or whole 11-word LDS rows (1) -- or at 4 bits (0), on reads from no N to mostly N's, a quarter of them in a
     repeat-rich reference, ragged lengths included: SMEMs, counts and backwardExt calls equal the
     oracle's."""
     monkeypatch.setenv("GB_FMI_Q2", q2)
