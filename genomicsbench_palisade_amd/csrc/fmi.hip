@@ -202,9 +202,9 @@ constexpr int kQBases = 152;
 constexpr int kQW = kQBases / 8;
 static_assert(kQW % 2 == 1, "odd row stride (LDS banks)");
 // kQ 2: the same reads staged at 2 bits per base (11 words per lane row, odd; 2.75 KB per wave
-// instead of 4.75) with the read's N positions in one register (pack_q2): the 2 KB saved hold two
-// more `prev` head entries at the same 16 waves per CU. A read with more than four N's goes to the
-// heavy pass when it is taken.
+// instead of 4.75) with the read's N positions in one register (pack_npos): the 2 KB saved hold two
+// more `prev` head entries at the same 16 waves per CU. A read with more than four N's reads its
+// bases from qdb instead.
 constexpr int kQW2 = 11;
 static_assert(kQW2 * 16 >= kQBases && kQW2 % 2 == 1, "2-bit rows: every base, odd stride");
 // kQ 3 (default): the first 128 bases' 2-bit codes in LDS (8 words, 2 KB per wave) and bases
@@ -218,9 +218,9 @@ static_assert(kQW3 * 16 + 32 >= kQBases, "2-bit split rows: every base");
 // wave-interleaved scratch. List index p of a list whose forward phase pushed n entries is push
 // k = n - 1 - p, kept in LDS slot k & (kTop - 1) = (c - p) & (kTop - 1) with c = n - 1: during the
 // forward phase the slots hold the last kTop pushes (a push evicts the one kTop before it to its
-// scratch position), and the compaction writes r'[q] into r[q]'s slot, already read. 1 KB per wave
-// per entry beside the staged read codes (kQ 3: eight entries and 2 KB of codes, 16 waves per CU).
-// slot of a ring of N entries (N a power of two: a mask; 5-7: an unsigned modulo, x >= 0)
+// scratch position), and the compaction writes r'[q] into r[q]'s slot, already read. 8 KB per wave
+// beside the 5.25 KB of staged read codes: 12 waves per CU still fit.
+// slot of a ring of N entries (N a power of two: a mask; 6: an unsigned modulo, x >= 0)
 template <int N>
 __device__ __forceinline__ int ring_slot(int x) {
   if constexpr ((N & (N - 1)) == 0)
@@ -229,9 +229,7 @@ __device__ __forceinline__ int ring_slot(int x) {
     return (int)((unsigned)x % (unsigned)N);
 }
 
-// kQ: read codes 0 from qdb, 1 staged 4-bit, 2 staged 2-bit rows, 3 staged 2-bit split rows (default);
-// kTop 0: every entry in the scratch
-template <int kQ, int kTop>
+template <int kQ, int kTop>  // kQ: read codes 0 from qdb, 1 staged 4-bit, 2 staged 2-bit; kTop 0: every entry in the scratch
 __global__ __launch_bounds__(64) void smem_search(SearchArgs A) {
   constexpr bool kTopLds = kTop > 0;
   constexpr bool kLdsQ = kQ > 0;
