@@ -44,7 +44,7 @@ import ctypes
 if tsub.n:
     oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(tsub.arr), tsub.n, pr.ctypes.data, rf.ctypes.data, rd.ctypes.data, None, 1)
 ref = gen.fmi_reference(60_000, seed=5)
-codes, lens = gen.fmi_reads(ref, 1300, seed=bench.set_seed(args, 8, rank))
+codes, lens = gen.fmi_reads(ref, int(os.environ.get("GB_NREADS", "1300")), seed=bench.set_seed(args, 8, rank))
 rlo, rhi = shard.read_range(len(lens), rank, world)
 oi = fmi_util.OracleIndex(ref)
 fs, fbc, _ = oi.run(codes[rlo:rhi], lens[rlo:rhi], batch_size=512)
@@ -109,7 +109,10 @@ def test_balanced_ranges_properties():
     assert r[0][0] == 0 and r[-1][1] == 1 and sum(hi - lo for lo, hi in r) == 1
 
 
-def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shards_concatenate_to_the_full_result(tmp_path, world):
+    """world 2 and 4 (the driver's 8-GPU scaling run also takes N = 2 / 4 / 8): every rank's shard
+    of every leg, gathered, equals the 1-rank result, and rank_check catches a corrupted shard."""
     import oracle_lib
     from genomicsbench_palisade_amd import bsw, gen
     out = tmp_path / "gathered.json"
@@ -117,9 +120,10 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
     wf.write_text(WORKER)
     port = _free_port()
     procs = []
-    for rank in range(2):
-        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), GB_ROOT=ROOT, GB_OUT=str(out), OMP_NUM_THREADS="1")
+    nreads = 1300 if world == 2 else 2100  # whole 512-read batches for every rank
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), GB_ROOT=ROOT, GB_OUT=str(out), OMP_NUM_THREADS="1", GB_NREADS=str(nreads))
         procs.append(subprocess.Popen([sys.executable, str(wf)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     for p in procs:
@@ -130,20 +134,23 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
             pytest.fail("gloo worker timed out")
         assert p.returncode == 0, e[-3000:]
     got = json.load(open(out))
-    assert [g["max"] for g in got] == [2.0, 2.0] and [g["sum"] for g in got] == [30.0, 30.0]
+    cat = lambda key: sum((g[key] for g in got), [])  # noqa: E731
+    assert [g["max"] for g in got] == [float(world)] * world
+    assert [g["sum"] for g in got] == [10.0 * world * (world + 1) / 2] * world
     calls = gen.chain_dataset("small", num_calls=60, seed=3, median_n=200, max_n=3000)
     full = oracle_lib.chain_oracle(calls, 1)[0]
-    assert got[0]["range"][0] == 0 and got[0]["range"][1] == got[1]["range"][0] and got[1]["range"][1] == calls.ncalls
-    assert (np.array(got[0]["chain"] + got[1]["chain"], np.int32) == full).all()
+    rngs = [g["range"] for g in got]
+    assert rngs[0][0] == 0 and rngs[-1][1] == calls.ncalls and all(a[1] == b[0] for a, b in zip(rngs, rngs[1:]))
+    assert (np.array(cat("chain"), np.int32) == full).all()
     pairs = gen.bsw_pairs(500, seed=4)
     fb = oracle_lib.bsw_oracle(pairs, bsw.default_params(), 1)[0]
-    assert (np.array(got[0]["bsw"] + got[1]["bsw"], np.int32).reshape(-1, 6) == fb).all()
-    assert [g["timed_steps_ms"] for g in got] == [1.5, 1.5]
+    assert (np.array(cat("bsw"), np.int32).reshape(-1, 6) == fb).all()
+    assert [g["timed_steps_ms"] for g in got] == [1.5] * world
     # bench.rank_check: rank 0 holds the check; the corrupted rank-1 shard was caught on rank 0 only
     rc = got[0]["rank_check"]
-    assert rc["bit_exact"] and rc["per_rank_match"] == [True, True] and rc["units"] == calls.nanchors
-    assert got[1]["rank_check"] is None
-    assert [g["caught"] for g in got] == [True, False]
+    assert rc["bit_exact"] and rc["per_rank_match"] == [True] * world and rc["units"] == calls.nanchors
+    assert all(g["rank_check"] is None for g in got[1:])
+    assert [g["caught"] for g in got] == [True] + [False] * (world - 1)
     # phmm: testcase shards balanced by cells concatenate to the 1-rank results
     import ctypes
     from genomicsbench_palisade_amd._tc import TestcaseArray
@@ -152,17 +159,20 @@ def test_gloo_world2_shards_concatenate_to_the_full_result(tmp_path):
     oracle_lib.oracle().phmm_oracle_batch(ctypes.addressof(ta.arr), ta.n, pr.ctypes.data, rf.ctypes.data,
                                           rd.ctypes.data, None, 1)
     # phmm: the ranks' stratified pieces (1/2 of every batch) partition the job and gather back
-    idx = np.array(got[0]["tidx"] + got[1]["tidx"])
+    idx = np.array(cat("tidx"))
     assert (np.sort(idx) == np.arange(ta.n)).all()
     gathered = np.zeros(ta.n)
-    gathered[idx] = np.array(got[0]["phmm"] + got[1]["phmm"])
+    gathered[idx] = np.array(cat("phmm"))
     assert (gathered.view(np.uint64) == pr.view(np.uint64)).all()
     # fmi: whole 512-read batches per rank; SMEM lists and per-batch counts concatenate
     import fmi_util
     ref = gen.fmi_reference(60_000, seed=5)
-    codes, lens = gen.fmi_reads(ref, 1300, seed=8)
+    codes, lens = gen.fmi_reads(ref, nreads, seed=8)
     fs, fbc, _ = fmi_util.OracleIndex(ref).run(codes, lens, batch_size=512)
-    assert got[0]["rrange"] == [0, 1024] and got[1]["rrange"] == [1024, 1300]
+    rr = [g["rrange"] for g in got]
+    assert rr[0][0] == 0 and rr[-1][1] == nreads and all(a[1] == b[0] and a[1] % 512 == 0 for a, b in zip(rr, rr[1:]))
+    if world == 2:
+        assert rr == [[0, 1024], [1024, 1300]]
     exp = [list(map(int, t)) for t in zip(fs["rid"], fs["m"], fs["n"], fs["k"], fs["l"], fs["s"])]
-    assert got[0]["fmi"] + got[1]["fmi"] == exp
-    assert got[0]["fmi_bc"] + got[1]["fmi_bc"] == fbc.tolist()
+    assert cat("fmi") == exp
+    assert cat("fmi_bc") == fbc.tolist()
